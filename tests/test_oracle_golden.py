@@ -1,0 +1,137 @@
+"""The oracle (C restatement of Generic) reproduces the reference's golden vectors.
+
+Fixtures: tests/golden/golden.json, produced by oracle/gen_golden.py from the reference's own
+Generic TUs (compiled in place from /root/reference/src).  Where the reference's Release
+(-Ofast) build and its strict twin disagree, the strict answer is the one the strict-IEEE
+restatement must reproduce (SURVEY.md §5 'Build numerics').
+"""
+import base64
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+
+
+def _cases(golden, big):
+    out = []
+    for c in golden["cases"]:
+        is_big = c["srcW"] * c["srcH"] > 4_000_000 or c["dstW"] * c["dstH"] > 4_000_000
+        if is_big == big:
+            out.append(c)
+    return out
+
+
+def _check(c):
+    src = ol.gen(c["gen"], c["srcW"], c["srcH"], c["seed"])
+    out = ol.run_oracle(c["method"], c["degree"], c["srcW"], c["srcH"], c["dstW"], c["dstH"], c["pxScale"], src)
+    want = c["fnv"] if c["ofast_strict_agree"] else c["fnv_strict"]
+    got = "%016x" % ol.fnv1a64(out)
+    if "out_b64" in c and c["ofast_strict_agree"]:
+        ref = np.frombuffer(base64.b64decode(c["out_b64"]), dtype=np.uint8).reshape(c["dstH"], c["dstW"])
+        diff = np.argwhere(ref != out)
+        assert diff.size == 0, "first diffs %s" % diff[:5].tolist()
+    assert got == want, c["id"]
+    assert out.ravel()[:8].tolist() == c["head"] or not c["ofast_strict_agree"]
+
+
+def test_golden_small(golden):
+    cases = _cases(golden, big=False)
+    assert len(cases) > 400
+    for c in cases:
+        _check(c)
+
+
+def test_golden_large(golden):
+    for c in _cases(golden, big=True):
+        _check(c)
+
+
+def test_golden_tables(golden):
+    n = 0
+    for c in golden["cases"]:
+        for axis, name in ((0, "tableX"), (1, "tableY")):
+            key = name if c[name + "_ofast_strict_agree"] else name + "_strict"
+            if key not in c:
+                continue
+            t = ol.oracle_tables(c["method"], c["degree"], c["srcW"], c["srcH"], c["dstW"], c["dstH"], c["pxScale"], axis)
+            assert list(t.shape) == c[name + "_shape"], c["id"]
+            assert t.ravel().tolist() == c[key], (c["id"], name)
+            n += 1
+    assert n > 800
+
+
+def test_known_tables_survey():
+    """SURVEY.md §8c quantised tables at the BASELINE shapes."""
+    x = ol.oracle_tables("lanczos", 3, 3840, 2160, 1920, 1080, 1, 0)
+    y = ol.oracle_tables("lanczos", 3, 3840, 2160, 1920, 1080, 1, 1)
+    assert x.tolist() == [[60, 247, -557, -1092, 2220, 7314, 7314, 2220, -1092, -557, 247, 60]]
+    assert y.tolist() == [[0, 1, -2, -4, 9, 28, 28, 9, -4, -2, 1, 0]]
+    assert ol.oracle_tables("area", 0, 7680, 4320, 1920, 1080, 1, 1).tolist() == [[64] * 4]
+    assert ol.oracle_tables("area", 0, 7680, 4320, 1920, 1080, 1, 0).tolist() == [[8192] * 4]
+    y2 = ol.oracle_tables("lanczos", 2, 640, 480, 320, 240, 1, 1)
+    assert y2.tolist() == [[-1, -3, 7, 29, 29, 7, -3, -1]]
+
+
+def test_known_answers_survey():
+    """SURVEY.md §8c sample pixels (d[0..3] / d[n/2] / d[n-1]) with generator G1."""
+    cases = [
+        (("lanczos", 2, 640, 480, 320, 240, 1), [85, 140, 89, 139], 86, 148),
+        (("area", 0, 1920, 1080, 960, 540, 1), [95, 155, 88, 148], 130, 73),
+        (("linear", 0, 640, 480, 1280, 960, 1), [0, 40, 119, 134], 34, 108),
+        (("lanczos", 3, 64, 48, 32, 24, 1), [84, 144, 89, 140], 144, 167),
+    ]
+    for (m, d, sw, sh, dw, dh, px), head, mid, last in cases:
+        out = ol.run_oracle(m, d, sw, sh, dw, dh, px, ol.gen("g1", sw, sh)).ravel()
+        assert out[:4].tolist() == head and out[out.size // 2] == mid and out[-1] == last
+
+
+def test_flat_inputs_stay_flat():
+    for m, d, sw, sh, dw, dh in [("lanczos", 3, 384, 216, 192, 108), ("area", 0, 768, 432, 192, 108),
+                                 ("linear", 0, 192, 108, 384, 216), ("lanczos", 2, 64, 48, 32, 24)]:
+        for v in (0, 255):
+            src = np.full((sh, sw), v, np.uint8)
+            out = ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)
+            assert (out == v).all()
+
+
+def test_strided_input_matches_packed():
+    sw, sh, dw, dh = 97, 61, 45, 33
+    src = ol.gen("noise", sw, sh, 7)
+    padded = np.zeros((sh, sw + 29), np.uint8)
+    padded[:, :sw] = src
+    a = ol.run_oracle("lanczos", 3, sw, sh, dw, dh, 1, src)
+    b = ol.run_oracle("lanczos", 3, sw, sh, dw, dh, 1, padded, dst_st=dw + 5)
+    assert (a == b).all()
+
+
+def _ref_clean(m, d, sw, sh, dw, dh):
+    import os
+    import subprocess
+    exe = os.path.join(ol.REF_DIR, "ref_asan_check")
+    if not os.path.exists(exe):
+        return True
+    r = subprocess.run([exe, str(ol.METHODS[m]), str(d), str(sw), str(sh), str(dw), str(dh), "1"],
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return r.returncode == 0
+
+
+@pytest.mark.skipif(not ol.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_matches_reference_random():
+    """Direct differential test against the compiled reference (build container only)."""
+    import random
+    rng = random.Random(1234)
+    for i in range(150):
+        m = rng.choice(["lanczos", "lanczos", "area"])
+        d = rng.randint(1, 4)
+        sw, sh = rng.randint(8, 200), rng.randint(8, 150)
+        dw = rng.randint(max(1, sw // 5), sw * 3) if m == "lanczos" else rng.randint(max(1, sw // 6), sw)
+        dh = rng.randint(max(1, sh // 5), sh * 3) if m == "lanczos" else rng.randint(max(1, sh // 6), sh)
+        if m == "area" and (sw % dw or sh % dh):
+            continue  # non-integer area ratios read past the buffer in the reference
+        if not _ref_clean(m, d, sw, sh, dw, dh):
+            continue  # the reference itself traps (zero border denominator) on this shape
+        src = ol.gen("noise", sw, sh, i)
+        a = ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)
+        b = ol.run_ref(m, d, sw, sh, dw, dh, 1, src, strict=True)
+        assert (a == b).all(), (m, d, sw, sh, dw, dh)
