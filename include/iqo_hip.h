@@ -1,0 +1,124 @@
+/*
+ * iqo_hip.h -- C ABI of the MI355X (gfx950) resize backend for libiqo's hot path.
+ *
+ * This is the drop-in boundary.  It replaces the per-arch implementation SPI of the reference
+ * (the `I*ResizerImpl` interface + `*ResizerImpl_new<Arch>()` factories) with plain C entry
+ * points: no C++ or torch types, only pointers, sizes, an opaque plan and an int status.
+ *
+ *   reference (read-only, /root/reference)                  replaced by
+ *   -------------------------------------------------------  ---------------------------------
+ *   LanczosResizerImpl_new<Arch>() + init()                  iqo_hip_plan_lanczos()
+ *       src/IQOLanczosResizerImpl.hpp:10-29,65-75;
+ *       src/IQOLanczosResizerImpl_Generic.cpp:291-339
+ *   AreaResizerImpl_new<Arch>() + init()                     iqo_hip_plan_area()
+ *       src/IQOAreaResizerImpl.hpp:10-27; src/IQOAreaResizerImpl_Generic.cpp:174-220
+ *   LinearResizerImpl_new<Arch>() + init()                   iqo_hip_plan_linear()
+ *       src/IQOLinearResizerImpl.hpp:10-27; src/IQOLinearResizerImpl_Generic.cpp:157-191
+ *   I*ResizerImpl::resize(srcSt, src, dstSt, dst)            iqo_hip_resize()  (host pointers)
+ *       src/IQOLanczosResizerImpl_Generic.cpp:369-454 etc.   iqo_hip_resize_device() (batched,
+ *                                                            device pointers, async on a stream)
+ *   delete m_Impl  (src/IQOLanczosResizer.cpp:39-42)         iqo_hip_plan_destroy()
+ *   HWCap CPUID dispatch (src/IQOHWCap.cpp:32-53)            iqo_hip_available()
+ *
+ * Semantics: output bytes are identical to the reference's Generic implementation
+ * (IQO*ResizerImpl_Generic) for the same inputs.  All functions return IQO_HIP_OK (0) or a
+ * negative status; the library never falls back to a CPU path.
+ *
+ * Threading: a plan may be used from one host thread at a time (like the reference impl, whose
+ * work row makes it non-re-entrant, IQOLanczosResizerImpl_Generic.cpp:279); distinct plans are
+ * independent.  Device-pointer calls are asynchronous on `stream` (a hipStream_t, or NULL for
+ * the default stream).
+ */
+#ifndef IQO_HIP_H
+#define IQO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IQO_HIP_OK 0
+#define IQO_HIP_EINVAL (-1)     /* bad argument (zero size, bad degree, null pointer, ...) */
+#define IQO_HIP_ENODEV (-2)     /* no gfx950 device / HIP runtime unusable */
+#define IQO_HIP_ENOMEM (-3)     /* host or device allocation failed */
+#define IQO_HIP_EHIP (-4)       /* a HIP runtime call or kernel launch failed */
+#define IQO_HIP_EUNSUP (-5)     /* shape or layout not supported (e.g. > 65535 frames) */
+
+enum { IQO_METHOD_LANCZOS = 0, IQO_METHOD_AREA = 1, IQO_METHOD_LINEAR = 2 };
+
+/* Kernel families a plan can dispatch to (iqo_hip_plan_desc.kernel). */
+enum {
+    IQO_KERNEL_GENERAL = 0,     /* any shape: one workgroup per output row, LDS work row */
+    IQO_KERNEL_LANCZOS_STREAM = 1, /* integer ratio, 1 phase: row-band walker, register window */
+    IQO_KERNEL_AREA_INT = 2,    /* integer ratio area */
+    IQO_KERNEL_LINEAR_UP2 = 3   /* exact 2x bilinear upsampling */
+};
+
+typedef struct iqo_hip_plan iqo_hip_plan;
+
+typedef struct {
+    int method;
+    int device;
+    size_t srcW, srcH, dstW, dstH;
+    int tapsX, tapsY;       /* reference coefficient counts (m_NumCoefsX/Y) */
+    int phasesX, phasesY;   /* reference table counts (m_NumTablesX/Y) */
+    int kernel;             /* IQO_KERNEL_* used for full frames with aligned layouts */
+    int bandsPerFrame;      /* fast-path row bands per frame (tuning) */
+} iqo_hip_plan_desc;
+
+/* Number of usable gfx950 devices (0 when none or the runtime is unusable). */
+int iqo_hip_available(void);
+
+/* Plan = coefficient tables + index maps built on the host and uploaded once to `device`. */
+int iqo_hip_plan_lanczos(unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                         size_t pxScale, int device, iqo_hip_plan **out);
+int iqo_hip_plan_area(size_t srcW, size_t srcH, size_t dstW, size_t dstH, int device, iqo_hip_plan **out);
+int iqo_hip_plan_linear(size_t srcW, size_t srcH, size_t dstW, size_t dstH, int device, iqo_hip_plan **out);
+void iqo_hip_plan_destroy(iqo_hip_plan *plan);
+
+int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
+
+/* Options (tests / tuning): "force_general" (0/1), "bands" (row bands per frame, 0 = auto). */
+int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);
+
+/* Drop-in resize with HOST pointers (byte strides), synchronous: H2D, kernels, D2H. */
+int iqo_hip_resize(iqo_hip_plan *plan, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst);
+
+/* Batched resize of nFrames frames resident in device memory, asynchronous on `stream`.
+ * Frame f reads dSrc + f*srcFrameSt and writes dDst + f*dstFrameSt. */
+int iqo_hip_resize_device(iqo_hip_plan *plan, size_t nFrames, size_t srcSt, size_t srcFrameSt,
+                          const uint8_t *dSrc, size_t dstSt, size_t dstFrameSt, uint8_t *dDst,
+                          void *stream);
+
+/* Source rows [*srcRow0, *srcRow0 + *srcRows) that output rows [dstRow0, dstRow0 + dstRows)
+ * read (the halo of a row band).  Host-only, no device work. */
+int iqo_hip_band_src_rows(const iqo_hip_plan *plan, size_t dstRow0, size_t dstRows, size_t *srcRow0,
+                          size_t *srcRows);
+
+/* Row-band resize (multi-GPU sharding by output rows): computes global output rows
+ * [dstRow0, dstRow0 + dstRows) of each frame.  dSrcWindow points at global source row srcRow0
+ * (as returned by iqo_hip_band_src_rows, or any window containing it); dDstBand points at the
+ * band's first row.  Rows are computed with their GLOBAL indices, so a banded result is
+ * byte-identical to the unsharded one. */
+int iqo_hip_resize_band(iqo_hip_plan *plan, size_t nFrames, size_t dstRow0, size_t dstRows,
+                        size_t srcRow0, size_t srcSt, size_t srcFrameSt, const uint8_t *dSrcWindow,
+                        size_t dstSt, size_t dstFrameSt, uint8_t *dDstBand, void *stream);
+
+const char *iqo_hip_strerror(int status);
+const char *iqo_hip_version(void);
+
+/* Host-only table query (no GPU needed): the quantised coefficient table the plan would upload
+ * for `axis` (0 = X, 1 = Y), widened to int32, phases x taps.  Returns phases*taps or < 0. */
+int iqo_host_tables(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                    size_t pxScale, int axis, int *nTaps, int *nPhases, int32_t *buf, size_t cap);
+
+/* Host-only: which kernel family a full-frame, 16-byte-aligned device call would use. */
+int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                        size_t pxScale);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,529 @@
+// abi.hip -- implementation of include/iqo_hip.h (the extern "C" boundary).
+//
+// A plan owns: the host Plan (tables + index maps, plan.cpp), their device copies, the chunk
+// table of the general kernel, the border tables of the Lanczos streamer, and (lazily) a stream
+// plus device staging buffers for the host-pointer entry point.  There is no CPU fallback:
+// any HIP failure is returned as a negative status.
+#include "iqo_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "kernels.hpp"
+#include "plan.hpp"
+
+using iqo_amd::AxisPlan;
+using iqo_amd::CoordInfo;
+using iqo_amd::Plan;
+
+struct iqo_hip_plan {
+    Plan p;
+    int device = 0;
+    int4 *dX = nullptr, *dY = nullptr, *dChunks = nullptr;
+    int *dTabX = nullptr, *dTabY = nullptr, *dBorder = nullptr;
+    int nChunks = 0, ldsInts = 0;
+    bool forceGeneral = false;
+    int bands = 0;
+    hipStream_t stream = nullptr;
+    uint8_t *stageSrc = nullptr, *stageDst = nullptr;
+    size_t stageSrcCap = 0, stageDstCap = 0;
+};
+
+namespace {
+
+constexpr int kChunkOut = 256;     // outputs per general-kernel chunk (= workgroup size)
+constexpr int kChunkLds = 8192;    // max work-row ints per chunk (32 KiB LDS)
+
+class DeviceGuard {  // restore the caller's current device
+public:
+    explicit DeviceGuard(int dev)
+    {
+        ok_ = hipGetDevice(&prev_) == hipSuccess && hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard()
+    {
+        if (ok_)
+            (void)hipSetDevice(prev_);
+    }
+    bool ok() const { return ok_; }
+
+private:
+    int prev_ = 0;
+    bool ok_ = false;
+};
+
+bool is_gfx950(int dev)
+{
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+        return false;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+template <typename T>
+int upload(T **dptr, const T *src, size_t n)
+{
+    if (n == 0)
+        n = 1;
+    if (hipMalloc(reinterpret_cast<void **>(dptr), n * sizeof(T)) != hipSuccess)
+        return IQO_HIP_ENOMEM;
+    if (src && hipMemcpy(*dptr, src, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+        return IQO_HIP_EHIP;
+    return IQO_HIP_OK;
+}
+
+// Source-column interval [a, b) that output column x reads (general kernel).
+void column_span(const Plan &p, int x, int *a, int *b)
+{
+    const CoordInfo &c = p.x.coord[static_cast<size_t>(x)];
+    const int W = p.srcW;
+    if (c.kind == iqo_amd::kIdentity) {
+        *a = c.srcO;
+        *b = c.srcO + 1;
+    } else if (p.method == iqo_amd::kLinear && c.kind != iqo_amd::kMain) {
+        *a = c.kind == iqo_amd::kBorderLo ? 0 : W - 1;
+        *b = *a + 1;
+    } else if (p.method == iqo_amd::kLinear) {
+        *a = std::max(0, std::min(c.srcO, W - 1));
+        *b = std::max(0, std::min(c.srcO + 1, W - 1)) + 1;
+    } else {
+        *a = std::max(0, std::min(c.srcO, W - 1));
+        *b = std::max(*a + 1, std::min(c.srcO + p.x.taps, W));
+    }
+}
+
+int build_chunks(const Plan &p, std::vector<int4> *chunks, int *ldsInts)
+{
+    chunks->clear();
+    *ldsInts = 1;
+    int x = 0;
+    while (x < p.dstW) {
+        int lo, hi;
+        column_span(p, x, &lo, &hi);
+        if (hi - lo > kChunkLds)
+            return IQO_HIP_EUNSUP;
+        int xe = x + 1;
+        while (xe < p.dstW && xe - x < kChunkOut) {
+            int a, b;
+            column_span(p, xe, &a, &b);
+            int nlo = std::min(lo, a), nhi = std::max(hi, b);
+            if (nhi - nlo > kChunkLds)
+                break;
+            lo = nlo;
+            hi = nhi;
+            ++xe;
+        }
+        chunks->push_back(make_int4(x, xe, lo, hi));
+        *ldsInts = std::max(*ldsInts, hi - lo);
+        x = xe;
+    }
+    return IQO_HIP_OK;
+}
+
+void free_plan(iqo_hip_plan *h)
+{
+    (void)hipFree(h->dX);
+    (void)hipFree(h->dY);
+    (void)hipFree(h->dChunks);
+    (void)hipFree(h->dTabX);
+    (void)hipFree(h->dTabY);
+    (void)hipFree(h->dBorder);
+    (void)hipFree(h->stageSrc);
+    (void)hipFree(h->stageDst);
+    if (h->stream)
+        (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+std::vector<int4> coord_records(const AxisPlan &a)
+{
+    std::vector<int4> v(a.coord.size());
+    for (size_t i = 0; i < v.size(); ++i)
+        v[i] = make_int4(a.coord[i].srcO, a.coord[i].tabOff, a.coord[i].kind, a.coord[i].aux);
+    return v;
+}
+
+int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t dw, size_t dh, size_t px,
+              int device, iqo_hip_plan **out)
+{
+    if (!out)
+        return IQO_HIP_EINVAL;
+    *out = nullptr;
+    iqo_hip_plan *h = new (std::nothrow) iqo_hip_plan();
+    if (!h)
+        return IQO_HIP_ENOMEM;
+    std::string err;
+    if (!iqo_amd::build_plan(m, degree, sw, sh, dw, dh, px, &h->p, &err)) {
+        delete h;
+        return IQO_HIP_EINVAL;
+    }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count || !is_gfx950(device)) {
+        delete h;
+        return IQO_HIP_ENODEV;
+    }
+    h->device = device;
+    DeviceGuard guard(device);
+    if (!guard.ok()) {
+        delete h;
+        return IQO_HIP_ENODEV;
+    }
+    std::vector<int4> chunks;
+    int rc = build_chunks(h->p, &chunks, &h->ldsInts);
+    if (rc) {
+        delete h;
+        return rc;
+    }
+    h->nChunks = static_cast<int>(chunks.size());
+    std::vector<int4> xr = coord_records(h->p.x), yr = coord_records(h->p.y);
+    std::vector<int> border(64, 0);
+    const iqo_amd::FastLanczos &f = h->p.flz;
+    for (size_t i = 0; i < f.denoYTop.size() && i < 16; ++i)
+        border[i] = f.denoYTop[i];
+    for (size_t i = 0; i < f.denoYBot.size() && i < 16; ++i)
+        border[16 + i] = f.denoYBot[i];
+    for (size_t i = 0; i < f.dXLeft.size() && i < 16; ++i)
+        border[32 + i] = f.dXLeft[i];
+    for (size_t i = 0; i < f.dXRight.size() && i < 16; ++i)
+        border[48 + i] = f.dXRight[i];
+    if ((rc = upload(&h->dX, xr.data(), xr.size())) || (rc = upload(&h->dY, yr.data(), yr.size())) ||
+        (rc = upload(&h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
+        (rc = upload(&h->dTabY, h->p.y.table.data(), h->p.y.table.size())) ||
+        (rc = upload(&h->dChunks, chunks.data(), chunks.size())) ||
+        (rc = upload(&h->dBorder, border.data(), border.size()))) {
+        free_plan(h);
+        return rc;
+    }
+    *out = h;
+    return IQO_HIP_OK;
+}
+
+uint32_t pair16(int lo, int hi) { return (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16); }
+
+bool aligned(const void *p, size_t a, size_t st, size_t fst)
+{
+    return (reinterpret_cast<uintptr_t>(p) % a) == 0 && (st % a) == 0 && (fst % a) == 0;
+}
+
+int auto_bands(int rows, int frames)
+{
+    // Enough row bands to keep ~8 workgroups resident per CU on 256 CUs across the batch,
+    // while keeping bands tall (the 2-row halo per band is re-read).
+    const int target = 2048;
+    int bands = std::max(1, (target + frames - 1) / frames);
+    return std::max(1, std::min(bands, rows / 32 > 0 ? rows / 32 : 1));
+}
+
+int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t srcRow0, size_t srcSt,
+             size_t srcFrameSt, const uint8_t *src, size_t dstSt, size_t dstFrameSt, uint8_t *dst, hipStream_t s)
+{
+    const Plan &p = h->p;
+    if (!src || !dst || srcSt < static_cast<size_t>(p.srcW) || dstSt < static_cast<size_t>(p.dstW))
+        return IQO_HIP_EINVAL;
+    if (r0 + rows > static_cast<size_t>(p.dstH) || srcRow0 >= static_cast<size_t>(p.srcH))
+        return IQO_HIP_EINVAL;
+    if (rows == 0 || nFrames == 0)
+        return IQO_HIP_OK;
+    DeviceGuard guard(h->device);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+
+    int kernel = h->forceGeneral ? IQO_KERNEL_GENERAL : p.kernel;
+    if (kernel == IQO_KERNEL_LANCZOS_STREAM && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.flz.KX, dstSt, dstFrameSt)))
+        kernel = IQO_KERNEL_GENERAL;
+    if (kernel == IQO_KERNEL_AREA_INT && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.far.KX, dstSt, dstFrameSt)))
+        kernel = IQO_KERNEL_GENERAL;
+    if (kernel == IQO_KERNEL_LINEAR_UP2 && !(aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 16, dstSt, dstFrameSt)))
+        kernel = IQO_KERNEL_GENERAL;
+
+    const int rb = static_cast<int>(r0), re = static_cast<int>(r0 + rows);
+    for (size_t f0 = 0; f0 < nFrames; f0 += 65535) {
+        iqo_amd::Io io;
+        io.frames = static_cast<int>(std::min<size_t>(65535, nFrames - f0));
+        io.src = src + f0 * srcFrameSt;
+        io.srcSt = static_cast<int64_t>(srcSt);
+        io.srcFrameSt = static_cast<int64_t>(srcFrameSt);
+        io.srcRow0 = static_cast<int>(srcRow0);
+        io.dst = dst + f0 * dstFrameSt;
+        io.dstSt = static_cast<int64_t>(dstSt);
+        io.dstFrameSt = static_cast<int64_t>(dstFrameSt);
+        io.dstRow0 = rb;
+        hipError_t e = hipSuccess;
+        if (kernel == IQO_KERNEL_LANCZOS_STREAM) {
+            iqo_amd::LanczosDev l{};
+            const iqo_amd::FastLanczos &f = p.flz;
+            l.KY = f.KY;
+            l.KX = f.KX;
+            l.NY = f.NY;
+            l.NXP = f.NXP;
+            l.offX = f.offX;
+            l.srcW = p.srcW;
+            l.srcH = p.srcH;
+            l.dstW = p.dstW;
+            l.dstH = p.dstH;
+            l.offY = f.offY;
+            for (int i = 0; i < f.NY; ++i)
+                l.cy[i] = pair16(f.cy[i], f.cy[i]);
+            for (int i = 0; i < f.NXP / 2; ++i)
+                l.cx[i] = pair16(f.cx[2 * i], f.cx[2 * i + 1]);
+            l.mainBeginY = f.mainBeginY;
+            l.mainEndY = f.mainEndY;
+            l.mainBeginX = f.mainBeginX;
+            l.mainEndX = f.mainEndX;
+            l.border = h->dBorder;
+            int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
+            e = iqo_amd::launch_lanczos_stream(l, io, rb, re, bands, s);
+        } else if (kernel == IQO_KERNEL_AREA_INT) {
+            iqo_amd::AreaDev a{};
+            a.KY = p.far.KY;
+            a.KX = p.far.KX;
+            a.srcW = p.srcW;
+            a.dstW = p.dstW;
+            for (int i = 0; i < a.KY; ++i)
+                a.cy[i] = pair16(p.far.cy[i], p.far.cy[i]);
+            for (int i = 0; i < a.KX / 2; ++i)
+                a.cx[i] = pair16(p.far.cx[2 * i], p.far.cx[2 * i + 1]);
+            e = iqo_amd::launch_area_int(a, io, rb, re, s);
+        } else if (kernel == IQO_KERNEL_LINEAR_UP2) {
+            iqo_amd::LinearDev l{};
+            l.srcW = p.srcW;
+            l.srcH = p.srcH;
+            l.dstW = p.dstW;
+            l.dstH = p.dstH;
+            for (int q = 0; q < 2; ++q) {
+                l.cx[q] = pair16(p.fln.cx[q][0], p.fln.cx[q][1]);
+                l.cy[q] = pair16(p.fln.cy[q][0], p.fln.cy[q][1]);
+            }
+            e = iqo_amd::launch_linear_up2(l, io, rb, re, s);
+        } else {
+            iqo_amd::GeneralDev g{};
+            g.method = p.method;
+            g.srcW = p.srcW;
+            g.srcH = p.srcH;
+            g.dstW = p.dstW;
+            g.nX = p.x.taps;
+            g.nY = p.y.taps;
+            g.xInfo = h->dX;
+            g.yInfo = h->dY;
+            g.tabX = h->dTabX;
+            g.tabY = h->dTabY;
+            g.chunks = h->dChunks;
+            g.nChunks = h->nChunks;
+            g.ldsInts = h->ldsInts;
+            e = iqo_amd::launch_general(g, io, rb, re, s);
+        }
+        if (e != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
+    return IQO_HIP_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int iqo_hip_available(void)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess)
+        return 0;
+    int n = 0;
+    for (int d = 0; d < count; ++d)
+        n += is_gfx950(d) ? 1 : 0;
+    return n;
+}
+
+int iqo_hip_plan_lanczos(unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH, size_t pxScale,
+                         int device, iqo_hip_plan **out)
+{
+    return make_plan(iqo_amd::kLanczos, degree, srcW, srcH, dstW, dstH, pxScale, device, out);
+}
+
+int iqo_hip_plan_area(size_t srcW, size_t srcH, size_t dstW, size_t dstH, int device, iqo_hip_plan **out)
+{
+    return make_plan(iqo_amd::kArea, 0, srcW, srcH, dstW, dstH, 1, device, out);
+}
+
+int iqo_hip_plan_linear(size_t srcW, size_t srcH, size_t dstW, size_t dstH, int device, iqo_hip_plan **out)
+{
+    return make_plan(iqo_amd::kLinear, 0, srcW, srcH, dstW, dstH, 1, device, out);
+}
+
+void iqo_hip_plan_destroy(iqo_hip_plan *plan)
+{
+    if (!plan)
+        return;
+    DeviceGuard guard(plan->device);
+    free_plan(plan);
+}
+
+int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
+{
+    if (!h || !d)
+        return IQO_HIP_EINVAL;
+    d->method = h->p.method;
+    d->device = h->device;
+    d->srcW = static_cast<size_t>(h->p.srcW);
+    d->srcH = static_cast<size_t>(h->p.srcH);
+    d->dstW = static_cast<size_t>(h->p.dstW);
+    d->dstH = static_cast<size_t>(h->p.dstH);
+    d->tapsX = h->p.x.taps;
+    d->tapsY = h->p.y.taps;
+    d->phasesX = h->p.x.phases;
+    d->phasesY = h->p.y.phases;
+    d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL : h->p.kernel;
+    d->bandsPerFrame = h->bands;
+    return IQO_HIP_OK;
+}
+
+int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
+{
+    if (!h || !key)
+        return IQO_HIP_EINVAL;
+    if (!std::strcmp(key, "force_general")) {
+        h->forceGeneral = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "bands")) {
+        if (value < 0)
+            return IQO_HIP_EINVAL;
+        h->bands = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    return IQO_HIP_EINVAL;
+}
+
+int iqo_hip_resize_device(iqo_hip_plan *h, size_t nFrames, size_t srcSt, size_t srcFrameSt, const uint8_t *dSrc,
+                          size_t dstSt, size_t dstFrameSt, uint8_t *dDst, void *stream)
+{
+    if (!h)
+        return IQO_HIP_EINVAL;
+    return run_band(h, nFrames, 0, static_cast<size_t>(h->p.dstH), 0, srcSt, srcFrameSt, dSrc, dstSt, dstFrameSt,
+                    dDst, static_cast<hipStream_t>(stream));
+}
+
+int iqo_hip_band_src_rows(const iqo_hip_plan *h, size_t dstRow0, size_t dstRows, size_t *srcRow0, size_t *srcRows)
+{
+    if (!h || !srcRow0 || !srcRows || dstRow0 + dstRows > static_cast<size_t>(h->p.dstH))
+        return IQO_HIP_EINVAL;
+    int s0, s1;
+    iqo_amd::band_src_rows(h->p, static_cast<int>(dstRow0), static_cast<int>(dstRow0 + dstRows), &s0, &s1);
+    *srcRow0 = static_cast<size_t>(s0);
+    *srcRows = static_cast<size_t>(s1 - s0);
+    return IQO_HIP_OK;
+}
+
+int iqo_hip_resize_band(iqo_hip_plan *h, size_t nFrames, size_t dstRow0, size_t dstRows, size_t srcRow0, size_t srcSt,
+                        size_t srcFrameSt, const uint8_t *dSrcWindow, size_t dstSt, size_t dstFrameSt, uint8_t *dDstBand,
+                        void *stream)
+{
+    if (!h)
+        return IQO_HIP_EINVAL;
+    return run_band(h, nFrames, dstRow0, dstRows, srcRow0, srcSt, srcFrameSt, dSrcWindow, dstSt, dstFrameSt,
+                    dDstBand, static_cast<hipStream_t>(stream));
+}
+
+int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
+{
+    if (!h || !src || !dst)
+        return IQO_HIP_EINVAL;
+    const Plan &p = h->p;
+    if (srcSt < static_cast<size_t>(p.srcW) || dstSt < static_cast<size_t>(p.dstW))
+        return IQO_HIP_EINVAL;
+    DeviceGuard guard(h->device);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+    if (!h->stream && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+        return IQO_HIP_EHIP;
+    const size_t sPitch = (static_cast<size_t>(p.srcW) + 15) & ~size_t(15);
+    const size_t dPitch = (static_cast<size_t>(p.dstW) + 15) & ~size_t(15);
+    const size_t sBytes = sPitch * p.srcH, dBytes = dPitch * p.dstH;
+    if (sBytes > h->stageSrcCap) {
+        (void)hipFree(h->stageSrc);
+        h->stageSrc = nullptr;
+        h->stageSrcCap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&h->stageSrc), sBytes) != hipSuccess)
+            return IQO_HIP_ENOMEM;
+        h->stageSrcCap = sBytes;
+    }
+    if (dBytes > h->stageDstCap) {
+        (void)hipFree(h->stageDst);
+        h->stageDst = nullptr;
+        h->stageDstCap = 0;
+        if (hipMalloc(reinterpret_cast<void **>(&h->stageDst), dBytes) != hipSuccess)
+            return IQO_HIP_ENOMEM;
+        h->stageDstCap = dBytes;
+    }
+    if (hipMemcpy2DAsync(h->stageSrc, sPitch, src, srcSt, p.srcW, p.srcH, hipMemcpyHostToDevice, h->stream) != hipSuccess)
+        return IQO_HIP_EHIP;
+    int rc = run_band(h, 1, 0, static_cast<size_t>(p.dstH), 0, sPitch, sBytes, h->stageSrc, dPitch, dBytes,
+                      h->stageDst, h->stream);
+    if (rc)
+        return rc;
+    if (hipMemcpy2DAsync(dst, dstSt, h->stageDst, dPitch, p.dstW, p.dstH, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+        return IQO_HIP_EHIP;
+    if (hipStreamSynchronize(h->stream) != hipSuccess)
+        return IQO_HIP_EHIP;
+    return IQO_HIP_OK;
+}
+
+const char *iqo_hip_strerror(int status)
+{
+    switch (status) {
+    case IQO_HIP_OK:
+        return "ok";
+    case IQO_HIP_EINVAL:
+        return "invalid argument";
+    case IQO_HIP_ENODEV:
+        return "no usable gfx950 device";
+    case IQO_HIP_ENOMEM:
+        return "out of memory";
+    case IQO_HIP_EHIP:
+        return "HIP runtime or kernel launch failure";
+    case IQO_HIP_EUNSUP:
+        return "unsupported shape or layout";
+    default:
+        return "unknown status";
+    }
+}
+
+const char *iqo_hip_version(void) { return "libiqo_amd 0.1 (gfx950)"; }
+
+int iqo_host_tables(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH, size_t pxScale,
+                    int axis, int *nTaps, int *nPhases, int32_t *buf, size_t cap)
+{
+    if (method < 0 || method > 2)
+        return IQO_HIP_EINVAL;
+    AxisPlan x, y;
+    std::string err;
+    if (!iqo_amd::build_tables(static_cast<iqo_amd::Method>(method), degree, srcW, srcH, dstW, dstH, pxScale, &x, &y, &err))
+        return IQO_HIP_EINVAL;
+    const AxisPlan &a = axis ? y : x;
+    if (nTaps)
+        *nTaps = a.taps;
+    if (nPhases)
+        *nPhases = a.phases;
+    if (buf && cap >= a.table.size())
+        std::memcpy(buf, a.table.data(), a.table.size() * sizeof(int32_t));
+    return static_cast<int>(a.table.size());
+}
+
+int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH, size_t pxScale)
+{
+    if (method < 0 || method > 2)
+        return IQO_HIP_EINVAL;
+    Plan p;
+    std::string err;
+    if (!iqo_amd::build_plan(static_cast<iqo_amd::Method>(method), degree, srcW, srcH, dstW, dstH, pxScale, &p, &err))
+        return IQO_HIP_EINVAL;
+    return p.kernel;
+}
+
+} // extern "C"

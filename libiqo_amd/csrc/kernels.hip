@@ -1,0 +1,609 @@
+// kernels.hip -- gfx950 (CDNA4) kernels for the separable U8 resize hot path.
+//
+// All arithmetic restates the reference's Generic fixed point exactly:
+//   Lanczos: int16 vertical accumulator with wrap (IQOLanczosResizerImpl_Generic.cpp:499-516),
+//            masked + renormalised borders (:464-490, :539-574), int32 horizontal dot product
+//            with (sum + 2^19) >> 20 rounding (:582-612).
+//   Area:    u16 vertical accumulator (IQOAreaResizerImpl_Generic.cpp:303-320), (sum+2^22)>>23.
+//   Linear:  u16 vertical blend, 1-px replicated borders (IQOLinearResizerImpl_Generic.cpp:290-407).
+// No MFMA: this is a memory-bound 1-D stencil.  The interior math uses packed 16-bit VALU
+// (v_pk_mad_u16 -- its low 16 bits ARE the reference's int16 wrap) for the vertical taps and
+// v_dot2 (int16 / u16 pairs, int32 accumulate) for the horizontal taps.
+#include "kernels.hpp"
+
+#include <utility>
+
+namespace iqo_amd {
+namespace {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte streaming load (source pixels are read once per band): nontemporal hint.
+__device__ __forceinline__ uint4 load16_nt(const uint8_t *p)
+{
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t c, uint32_t acc)
+{
+    u16x2 r = __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, c) + __builtin_bit_cast(u16x2, acc);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+__device__ __forceinline__ uint32_t pk_mul(uint32_t a, uint32_t c)
+{
+    u16x2 r = __builtin_bit_cast(u16x2, a) * __builtin_bit_cast(u16x2, c);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+__device__ __forceinline__ int sdot2(uint32_t a, uint32_t c, int acc)
+{
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, c), acc, false);
+}
+
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t c, uint32_t acc)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, c), acc, false);
+}
+
+// bytes b0..b3 of v -> (b0,b1) and (b2,b3) as zero-extended u16 pairs
+__device__ __forceinline__ void unpack4(uint32_t v, uint32_t &lo, uint32_t &hi)
+{
+    lo = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
+    hi = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
+}
+
+__device__ __forceinline__ void unpack16(uint4 v, uint32_t (&w)[8])
+{
+    unpack4(v.x, w[0], w[1]);
+    unpack4(v.y, w[2], w[3]);
+    unpack4(v.z, w[4], w[5]);
+    unpack4(v.w, w[6], w[7]);
+}
+
+// Exact C (truncating) int32 division n / d for |n| < 2^31, d != 0, |quotient| < 2^22:
+// float reciprocal estimate of the magnitudes, then one-step integer correction.
+__device__ __forceinline__ int exact_div(int n, int d)
+{
+    if (d == 0)
+        return 0;  // the reference traps (SIGFPE); such shapes are outside parity
+    uint32_t an = n < 0 ? 0u - static_cast<uint32_t>(n) : static_cast<uint32_t>(n);
+    uint32_t ad = d < 0 ? 0u - static_cast<uint32_t>(d) : static_cast<uint32_t>(d);
+    float r = __builtin_amdgcn_rcpf(static_cast<float>(ad));
+    uint32_t q = static_cast<uint32_t>(static_cast<float>(an) * r);
+    int64_t rem = static_cast<int64_t>(an) - static_cast<int64_t>(q) * ad;
+    while (rem < 0) {
+        --q;
+        rem += ad;
+    }
+    while (rem >= static_cast<int64_t>(ad)) {
+        ++q;
+        rem -= ad;
+    }
+    return ((n ^ d) < 0) ? -static_cast<int>(q) : static_cast<int>(q);
+}
+
+__device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+// Compile-time loop: f(std::integral_constant<int, 0>) ... f(integral_constant<int, N-1>), so
+// register-array indices derived from the induction variable are constants (no scratch).
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>)
+{
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f)
+{
+    static_for_impl(static_cast<F &&>(f), std::make_integer_sequence<int, N>{});
+}
+
+// ================================================================ general kernel
+
+enum { KMAIN = 0, KLO = 1, KHI = 2, KID = 3 };
+
+struct GeneralArgs {
+    GeneralDev g;
+    Io io;
+    int rowBegin;
+};
+
+__device__ __forceinline__ int src_px(const GeneralArgs &a, const uint8_t *srcF, int row, int col)
+{
+    return srcF[static_cast<int64_t>(row - a.io.srcRow0) * a.io.srcSt + col];
+}
+
+// Vertical value at (row record yi, source column col): the reference's work[col].
+__device__ int y_value(const GeneralArgs &a, const uint8_t *srcF, int4 yi, int col)
+{
+    const GeneralDev &g = a.g;
+    if (g.method == 0) {  // Lanczos, int16 work row
+        if (yi.z == KID)
+            return static_cast<int16_t>(static_cast<uint16_t>(src_px(a, srcF, yi.x, col) * 64));
+        if (yi.z == KMAIN) {
+            int16_t acc = 0;  // resizeYmain :509-515
+            for (int i = 0; i < g.nY; ++i)
+                acc = static_cast<int16_t>(acc + src_px(a, srcF, yi.x + i, col) * g.tabY[yi.y + i]);
+            return acc;
+        }
+        int16_t nume = 0;  // resizeYborder :477-489
+        for (int i = 0; i < g.nY; ++i) {
+            int r = yi.x + i;
+            if (r >= 0 && r < g.srcH)
+                nume = static_cast<int16_t>(nume + src_px(a, srcF, r, col) * g.tabY[yi.y + i]);
+        }
+        return static_cast<int16_t>(exact_div(static_cast<int>(nume) * 64, yi.w));
+    }
+    if (yi.z == KID)
+        return static_cast<uint16_t>(src_px(a, srcF, yi.x, col) * 256);
+    if (g.method == 1) {  // Area, u16 work row (resizeYmain :313-319); weight-0 tap past the end clamped
+        uint16_t acc = 0;
+        for (int i = 0; i < g.nY; ++i) {
+            int r = min(yi.x + i, g.srcH - 1);
+            acc = static_cast<uint16_t>(acc + src_px(a, srcF, r, col) * g.tabY[yi.y + i]);
+        }
+        return acc;
+    }
+    // Linear (resize :241-281)
+    if (yi.z == KLO)
+        return static_cast<uint16_t>(src_px(a, srcF, 0, col) * 256);
+    if (yi.z == KHI)
+        return static_cast<uint16_t>(src_px(a, srcF, g.srcH - 1, col) * 256);
+    int r0 = max(0, min(yi.x, g.srcH - 1)), r1 = max(0, min(yi.x + 1, g.srcH - 1));
+    uint16_t acc = static_cast<uint16_t>(src_px(a, srcF, r0, col) * g.tabY[yi.y]);
+    acc = static_cast<uint16_t>(acc + src_px(a, srcF, r1, col) * g.tabY[yi.y + 1]);
+    return acc;
+}
+
+// Horizontal value at output column x from the LDS work row covering columns [lo, hi).
+__device__ int x_value(const GeneralArgs &a, const int *w, int lo, int hi, int x)
+{
+    const GeneralDev &g = a.g;
+    const int4 xi = g.xInfo[x];
+    auto W = [&](int col) { return w[max(0, min(col, hi - 1) - lo)]; };
+    if (g.method == 0) {
+        if (xi.z == KID)  // resizeX Y-only branch :520-527
+            return clamp255(static_cast<int16_t>((W(xi.x) + 32) >> 6));
+        if (xi.z == KMAIN) {  // resizeXmain :605-610
+            int sum = 0;
+            for (int i = 0; i < g.nX; ++i)
+                sum += W(xi.x + i) * g.tabX[xi.y + i];
+            return clamp255(static_cast<int16_t>((sum + (1 << 19)) >> 20));
+        }
+        int nume = 0;  // resizeXborder :563-572
+        for (int i = 0; i < g.nX; ++i) {
+            int col = xi.x + i;
+            if (col >= 0 && col < g.srcW)
+                nume += W(col) * g.tabX[xi.y + i];
+        }
+        return clamp255(static_cast<int16_t>(exact_div(nume + (1 << 19), xi.w * 64)));
+    }
+    if (xi.z == KID)
+        return clamp255(static_cast<int16_t>((W(xi.x) + 128) >> 8));
+    auto u16clamp = [](int v) {  // uint8(clamp<uint16_t>(0, 255, int16(v)))
+        uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(v));
+        return static_cast<int>(u > 255 ? 255 : u);
+    };
+    if (g.method == 1) {  // Area resizeXmain :349-367
+        int sum = 0;
+        for (int i = 0; i < g.nX; ++i)
+            sum += W(min(xi.x + i, g.srcW - 1)) * g.tabX[xi.y + i];
+        return u16clamp((sum + (1 << 22)) >> 23);
+    }
+    if (xi.z == KLO)  // Linear resizeXborder :355-366
+        return u16clamp((W(0) + 128) >> 8);
+    if (xi.z == KHI)
+        return u16clamp((W(g.srcW - 1) + 128) >> 8);
+    int c0 = max(0, min(xi.x, g.srcW - 1)), c1 = max(0, min(xi.x + 1, g.srcW - 1));
+    int sum = W(c0) * g.tabX[xi.y] + W(c1) * g.tabX[xi.y + 1];  // :400-405
+    return u16clamp((sum + (1 << 22)) >> 23);
+}
+
+__global__ __launch_bounds__(256) void general_kernel(GeneralArgs a)
+{
+    extern __shared__ __attribute__((aligned(16))) int wrow[];
+    const int y = a.rowBegin + static_cast<int>(blockIdx.x);
+    const uint8_t *srcF = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
+    uint8_t *dstRow = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt +
+                      static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt;
+    const int4 yi = a.g.yInfo[y];
+    for (int c = 0; c < a.g.nChunks; ++c) {
+        const int4 ch = a.g.chunks[c];
+        for (int col = ch.z + static_cast<int>(threadIdx.x); col < ch.w; col += static_cast<int>(blockDim.x))
+            wrow[col - ch.z] = y_value(a, srcF, yi, col);
+        __syncthreads();
+        const int x = ch.x + static_cast<int>(threadIdx.x);
+        if (x < ch.y)
+            dstRow[x] = static_cast<uint8_t>(x_value(a, wrow, ch.z, ch.w, x));
+        __syncthreads();
+    }
+}
+
+// ================================================================ Lanczos row-band streamer
+//
+// Workgroup = one row band of one frame, spanning the full source width: thread t owns source
+// columns [16t, 16t+16).  It walks the band's output rows top to bottom holding the NY source
+// rows of the vertical window in registers (unpacked to u16 pairs, a static ring: every source
+// row is fetched from HBM once per band with coalesced 16-B loads and unpacked once), prefetching
+// the next KY rows while it computes.  The vertical result (the reference's int16 work row) goes
+// to a double-buffered LDS row with zero pads, so the horizontal taps -- including the masked
+// border columns, whose invalid taps then read zero -- come from LDS with aligned 16-B reads.
+// Border rows/columns differ from the interior only by a per-row / per-column divisor
+// (renormalisation), applied where the reference applies it.
+
+struct LanczosArgs {
+    LanczosDev l;
+    Io io;
+    int rowBegin, rowEnd, rowsPerBand;
+};
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+constexpr int floor4(int v) { return v >= 0 ? (v / 4) * 4 : -(((-v) + 3) / 4) * 4; }
+constexpr int kPadW = 8;  // zero dwords left and right of each LDS work row
+
+template <int KY, int KX, int NY, int NXP, int OFFXD>
+__global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
+{
+    constexpr int OUTS = 16 / KX;
+    constexpr int U = NY / cgcd(NY, KY);
+    constexpr int D0 = floor4(OFFXD);
+    constexpr int LAST = OFFXD + (OUTS - 1) * KX / 2 + NXP / 2;
+    constexpr int NR = (LAST - D0 + 3) / 4;
+    static_assert(D0 >= -kPadW && D0 + 4 * NR - 8 <= kPadW, "LDS pad too small");
+    static_assert(OUTS == 8 || OUTS == 4, "");
+
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const LanczosDev &L = a.l;
+    const int t = static_cast<int>(threadIdx.x);
+    const int nthr = L.srcW >> 4;
+    const bool active = t < nthr;
+    const int rowDw = L.srcW >> 1;
+    const int BS = (rowDw + 2 * kPadW + 3) & ~3;
+
+    for (int i = t; i < 2 * BS; i += static_cast<int>(blockDim.x)) {
+        int j = i % BS;
+        if (j < kPadW || j >= kPadW + rowDw)
+            lds[i] = 0;
+    }
+
+    const int y0 = a.rowBegin + static_cast<int>(blockIdx.x) * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+
+    const uint8_t *srcF = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt + 16 * t;
+    uint8_t *dstF = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt + OUTS * t;
+    const int64_t srcSt = a.io.srcSt;
+    const int srcRow0 = a.io.srcRow0, srcH = L.srcH;
+
+    auto load_row = [&](int r) -> uint4 {
+        uint4 v = make_uint4(0u, 0u, 0u, 0u);
+        if (active && r >= 0 && r < srcH)
+            v = load16_nt(srcF + static_cast<int64_t>(r - srcRow0) * srcSt);
+        return v;
+    };
+
+    uint32_t win[NY][8];
+#pragma unroll
+    for (int i = 0; i < NY - KY; ++i)
+        unpack16(load_row(KY * y0 + L.offY + i), win[i]);
+    uint4 pre[KY];
+#pragma unroll
+    for (int j = 0; j < KY; ++j)
+        pre[j] = load_row(KY * y0 + L.offY + NY - KY + j);
+
+    for (int yb = y0; yb < y1; yb += U) {
+        static_for<U>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            const int yy = yb + u;
+            if (yy < y1) {
+#pragma unroll
+                for (int j = 0; j < KY; ++j)
+                    unpack16(pre[j], win[(u * KY + NY - KY + j) % NY]);
+                if (yy + 1 < y1) {
+#pragma unroll
+                    for (int j = 0; j < KY; ++j)
+                        pre[j] = load_row(KY * (yy + 1) + L.offY + NY - KY + j);
+                }
+                // ---- vertical taps (int16 wrap == low half of the packed u16 MAD)
+                uint32_t acc[8];
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    uint32_t s = pk_mul(win[(u * KY) % NY][c], L.cy[0]);
+#pragma unroll
+                    for (int i = 1; i < NY; ++i)
+                        s = pk_mad(win[(u * KY + i) % NY][c], L.cy[i], s);
+                    acc[c] = s;
+                }
+                if (yy < L.mainBeginY || yy >= L.mainEndY) {
+                    // border row: work = int16(int(nume) * 64 / deno)   (resizeYborder :487-489)
+                    const int den = yy < L.mainBeginY ? L.border[yy] : L.border[16 + yy - L.mainEndY];
+#pragma unroll
+                    for (int c = 0; c < 8; ++c) {
+                        int lo = static_cast<int16_t>(acc[c] & 0xffffu), hi = static_cast<int16_t>(acc[c] >> 16);
+                        lo = static_cast<uint16_t>(static_cast<int16_t>(exact_div(lo * 64, den)));
+                        hi = static_cast<uint16_t>(static_cast<int16_t>(exact_div(hi * 64, den)));
+                        acc[c] = static_cast<uint32_t>(lo) | (static_cast<uint32_t>(hi) << 16);
+                    }
+                }
+                uint32_t *row = lds + (yy & 1) * BS + kPadW;
+                if (active) {
+                    *reinterpret_cast<uint4 *>(row + 8 * t) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+                    *reinterpret_cast<uint4 *>(row + 8 * t + 4) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+                }
+                __syncthreads();
+                // ---- horizontal taps from LDS (int16 pairs . coefficient pairs -> int32)
+                uint32_t d[4 * NR];
+                const uint4 *b4 = reinterpret_cast<const uint4 *>(row + 8 * t + D0);
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    uint4 q = b4[r];
+                    d[4 * r + 0] = q.x;
+                    d[4 * r + 1] = q.y;
+                    d[4 * r + 2] = q.z;
+                    d[4 * r + 3] = q.w;
+                }
+                int sum[OUTS];
+#pragma unroll
+                for (int k = 0; k < OUTS; ++k) {
+                    int s = 1 << 19;
+#pragma unroll
+                    for (int p = 0; p < NXP / 2; ++p)
+                        s = sdot2(d[(KX * k) / 2 + OFFXD - D0 + p], L.cx[p], s);
+                    sum[k] = s >> 20;
+                    const int x = OUTS * t + k;
+                    if (x < L.mainBeginX)  // border column: int16((nume + 2^19) / (deno * 64))
+                        sum[k] = exact_div(s, L.border[32 + x]);
+                    else if (x >= L.mainEndX)
+                        sum[k] = exact_div(s, L.border[48 + x - L.mainEndX]);
+                    sum[k] = clamp255(static_cast<int16_t>(sum[k]));
+                }
+                if (active) {
+                    uint8_t *out = dstF + static_cast<int64_t>(yy - a.io.dstRow0) * a.io.dstSt;
+                    uint32_t w0 = sum[0] | (sum[1] << 8) | (sum[2] << 16) | (sum[3] << 24);
+                    if constexpr (OUTS == 8) {
+                        uint32_t w1 = sum[4] | (sum[5] << 8) | (sum[6] << 16) | (sum[7] << 24);
+                        *reinterpret_cast<uint2 *>(out) = make_uint2(w0, w1);
+                    } else {
+                        *reinterpret_cast<uint32_t *>(out) = w0;
+                    }
+                }
+            }
+        });
+    }
+}
+
+// ================================================================ Area integer ratio
+//
+// Thread = 16 source columns of one output row: KY coalesced 16-B row loads, packed u16 vertical
+// MACs, u16-pair dot products for the KX horizontal taps (all inside the thread's columns).
+
+struct AreaArgs {
+    AreaDev g;
+    Io io;
+    int rowBegin, rowEnd, groups;
+};
+
+template <int KX, int KYT>
+__global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
+{
+    constexpr int OUTS = 16 / KX;
+    const int KY = KYT ? KYT : a.g.KY;
+    const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t total = static_cast<int64_t>(a.rowEnd - a.rowBegin) * a.groups;
+    if (gid >= total)
+        return;
+    const int y = a.rowBegin + static_cast<int>(gid / a.groups);
+    const int gcol = static_cast<int>(gid % a.groups);
+    const uint8_t *s = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt +
+                       static_cast<int64_t>(KY * y - a.io.srcRow0) * a.io.srcSt + 16 * gcol;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll 4
+    for (int i = 0; i < KY; ++i) {
+        uint4 v = load16_nt(s + static_cast<int64_t>(i) * a.io.srcSt);
+        uint32_t w[8];
+        unpack16(v, w);
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            acc[c] = pk_mad(w[c], a.g.cy[i], acc[c]);
+    }
+    uint32_t out[OUTS];
+#pragma unroll
+    for (int k = 0; k < OUTS; ++k) {
+        uint32_t sum = 1u << 22;
+#pragma unroll
+        for (int p = 0; p < KX / 2; ++p)
+            sum = udot2(acc[(KX * k) / 2 + p], a.g.cx[p], sum);
+        int v = static_cast<int16_t>(static_cast<int>(sum) >> 23);
+        uint16_t u = static_cast<uint16_t>(v);
+        out[k] = u > 255 ? 255u : u;
+    }
+    uint8_t *d = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt +
+                 static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt + OUTS * gcol;
+    if constexpr (OUTS == 8) {
+        *reinterpret_cast<uint2 *>(d) = make_uint2(out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24),
+                                                   out[4] | (out[5] << 8) | (out[6] << 16) | (out[7] << 24));
+    } else if constexpr (OUTS == 4) {
+        *reinterpret_cast<uint32_t *>(d) = out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24);
+    } else if constexpr (OUTS == 2) {
+        *reinterpret_cast<uint16_t *>(d) = static_cast<uint16_t>(out[0] | (out[1] << 8));
+    } else {
+        d[0] = static_cast<uint8_t>(out[0]);
+    }
+}
+
+// ================================================================ exact 2x bilinear upsampler
+//
+// Thread = 16 output columns of one output row; it needs work columns [8t-1, 8t+8] of the two
+// source rows (interior: o = (y-1)>>1, phase y&1).  Bytes are gathered straight into
+// odd-aligned u16 pairs P_q = (8t-1+2q, 8t+2q); even pairs come from v_alignbit.
+
+struct LinearArgs {
+    LinearDev g;
+    Io io;
+    int rowBegin, rowEnd, groups;
+};
+
+__device__ __forceinline__ void gather_pairs(const uint8_t *row, int t, int srcW, uint32_t (&P)[5])
+{
+    // bytes [8t-4, 8t+12) as four dwords, clamped inside the row (clamped bytes feed only the
+    // replicated border columns, which do not read them)
+    int c0 = max(8 * t - 4, 0);
+    int c2 = min(8 * t + 8, srcW - 4);
+    uint32_t d0 = *reinterpret_cast<const uint32_t *>(row + c0);
+    uint2 d12 = *reinterpret_cast<const uint2 *>(row + 8 * t);
+    uint32_t d3 = *reinterpret_cast<const uint32_t *>(row + c2);
+    P[0] = __builtin_amdgcn_perm(d12.x, d0, 0x0c040c03u);
+    P[1] = __builtin_amdgcn_perm(0u, d12.x, 0x0c020c01u);
+    P[2] = __builtin_amdgcn_perm(d12.y, d12.x, 0x0c040c03u);
+    P[3] = __builtin_amdgcn_perm(0u, d12.y, 0x0c020c01u);
+    P[4] = __builtin_amdgcn_perm(d3, d12.y, 0x0c040c03u);
+}
+
+__global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
+{
+    const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t total = static_cast<int64_t>(a.rowEnd - a.rowBegin) * a.groups;
+    if (gid >= total)
+        return;
+    const LinearDev &g = a.g;
+    const int y = a.rowBegin + static_cast<int>(gid / a.groups);
+    const int t = static_cast<int>(gid % a.groups);
+    const uint8_t *srcF = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
+    auto row_ptr = [&](int r) { return srcF + static_cast<int64_t>(r - a.io.srcRow0) * a.io.srcSt; };
+
+    uint32_t W[5];  // work pairs (u16) at odd alignment
+    if (y == 0 || y == g.dstH - 1) {
+        // replicated first / last source row: work = src * 256 (:290-299)
+        uint32_t P[5];
+        gather_pairs(row_ptr(y == 0 ? 0 : g.srcH - 1), t, g.srcW, P);
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            W[q] = pk_mul(P[q], 0x01000100u);
+    } else {
+        const int o = (y - 1) >> 1;
+        const uint32_t c = g.cy[y & 1];
+        uint32_t P0[5], P1[5];
+        gather_pairs(row_ptr(o), t, g.srcW, P0);
+        gather_pairs(row_ptr(o + 1), t, g.srcW, P1);
+        const uint32_t c0 = (c & 0xffffu) * 0x10001u, c1 = (c >> 16) * 0x10001u;
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            W[q] = pk_mad(P1[q], c1, pk_mul(P0[q], c0));
+    }
+    uint32_t E[4];  // even-aligned pairs (8t+2q, 8t+2q+1)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        E[q] = __builtin_amdgcn_alignbit(W[q + 1], W[q], 16);
+
+    uint32_t outw[4];
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = 4 * j4 + jj;
+            const int r = (j - 1) >> 1;  // work column offset from 8t (floor)
+            const uint32_t pair = (r & 1) ? W[(r + 1) >> 1] : E[r >> 1];
+            uint32_t pairj = (j == 0) ? W[0] : pair;
+            uint32_t sum = udot2(pairj, g.cx[j & 1], 1u << 22);
+            uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(sum) >> 23));
+            uint32_t v = u > 255 ? 255u : u;
+            word |= v << (8 * jj);
+        }
+        outw[j4] = word;
+    }
+    // replicated border columns (:343-345, :360-365): x = 0 reads work[0], x = dstW-1 work[srcW-1]
+    if (t == 0) {
+        uint32_t w0 = W[0] >> 16;  // column 0 = high half of P_0 (columns -1, 0)
+        uint16_t u = static_cast<uint16_t>(static_cast<int16_t>((static_cast<int>(w0) + 128) >> 8));
+        outw[0] = (outw[0] & ~0xffu) | (u > 255 ? 255u : u);
+    }
+    if (t == a.groups - 1) {
+        uint32_t wl = W[4] & 0xffffu;  // column 8t+7 = srcW-1 = low half of P_4
+        uint16_t u = static_cast<uint16_t>(static_cast<int16_t>((static_cast<int>(wl) + 128) >> 8));
+        outw[3] = (outw[3] & 0x00ffffffu) | ((u > 255 ? 255u : static_cast<uint32_t>(u)) << 24);
+    }
+    uint8_t *d = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt +
+                 static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt + 16 * t;
+    *reinterpret_cast<uint4 *>(d) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+}
+
+} // namespace
+
+// ================================================================ launchers
+
+hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    GeneralArgs a{g, io, rowBegin};
+    dim3 grid(static_cast<unsigned>(rowEnd - rowBegin), static_cast<unsigned>(io.frames));
+    size_t lds = static_cast<size_t>(g.ldsInts) * sizeof(int);
+    hipLaunchKernelGGL(general_kernel, grid, dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
+bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)
+{
+    return KY == 2 && KX == 2 && ((NY == 10 && NXP == 14 && offX == -6) || (NY == 8 && NXP == 10 && offX == -4));
+}
+
+int lanczos_stream_block(int srcW) { return ((srcW / 16 + 63) / 64) * 64; }
+
+hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
+                                 hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    const int rows = rowEnd - rowBegin;
+    bands = max(1, min(bands, rows));
+    LanczosArgs a{l, io, rowBegin, rowEnd, (rows + bands - 1) / bands};
+    bands = (rows + a.rowsPerBand - 1) / a.rowsPerBand;
+    dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames));
+    dim3 block(static_cast<unsigned>(lanczos_stream_block(l.srcW)));
+    const int rowDw = l.srcW / 2;
+    const int BS = (rowDw + 2 * kPadW + 3) & ~3;
+    size_t lds = static_cast<size_t>(2 * BS) * sizeof(uint32_t);
+    if (l.NY == 10)
+        hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3>), grid, block, lds, s, a);
+    else
+        hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2>), grid, block, lds, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_area_int(const AreaDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    AreaArgs a{g, io, rowBegin, rowEnd, g.srcW / 16};
+    int64_t total = static_cast<int64_t>(rowEnd - rowBegin) * a.groups;
+    dim3 grid(static_cast<unsigned>((total + 255) / 256), static_cast<unsigned>(io.frames));
+    if (g.KX == 4 && g.KY == 4)
+        hipLaunchKernelGGL((area_int_kernel<4, 4>), grid, dim3(256), 0, s, a);
+    else if (g.KX == 2 && g.KY == 2)
+        hipLaunchKernelGGL((area_int_kernel<2, 2>), grid, dim3(256), 0, s, a);
+    else if (g.KX == 2)
+        hipLaunchKernelGGL((area_int_kernel<2, 0>), grid, dim3(256), 0, s, a);
+    else if (g.KX == 4)
+        hipLaunchKernelGGL((area_int_kernel<4, 0>), grid, dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((area_int_kernel<8, 0>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    LinearArgs a{g, io, rowBegin, rowEnd, g.dstW / 16};
+    int64_t total = static_cast<int64_t>(rowEnd - rowBegin) * a.groups;
+    dim3 grid(static_cast<unsigned>((total + 255) / 256), static_cast<unsigned>(io.frames));
+    hipLaunchKernelGGL(linear_up2_kernel, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+} // namespace iqo_amd

@@ -1,0 +1,64 @@
+// kernels.hpp -- launch interface of the gfx950 resize kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace iqo_amd {
+
+// A device-side view of one batched call: frame f reads src + f*srcFrameSt, whose row 0 is
+// GLOBAL source row srcRow0, and writes dst + f*dstFrameSt, whose row 0 is global row dstRow0.
+struct Io {
+    const uint8_t *src;
+    int64_t srcSt, srcFrameSt;
+    int srcRow0;
+    uint8_t *dst;
+    int64_t dstSt, dstFrameSt;
+    int dstRow0;
+    int frames;
+};
+
+// --- general kernel: one workgroup per output row; LDS work row built chunk by chunk.
+struct GeneralDev {
+    int method, srcW, srcH, dstW, nX, nY;
+    const int4 *xInfo, *yInfo;   // {srcO, tabOff, kind, aux} per dst column / row
+    const int *tabX, *tabY;      // quantised tables (int16 / u16 values widened)
+    const int4 *chunks;          // {xs, xe, lo, hi}
+    int nChunks;
+    int ldsInts;                 // work-row capacity (ints) of the largest chunk
+};
+hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
+
+// --- Lanczos row-band streamer (integer ratio, single phase).
+struct LanczosDev {
+    int KY, KX, NY, NXP, offX;
+    int srcW, srcH, dstW, dstH;
+    int offY;
+    uint32_t cy[16];             // (c, c) u16 pairs
+    uint32_t cx[16];             // (c_2p, c_2p+1) int16 pairs
+    int mainBeginY, mainEndY, mainBeginX, mainEndX;
+    const int *border;           // device: [0,16) denoYTop, [16,32) denoYBot, [32,48) dXLeft, [48,64) dXRight
+};
+bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
+hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
+                                 hipStream_t s);
+int lanczos_stream_block(int srcW);
+
+// --- Area integer-ratio kernel.
+struct AreaDev {
+    int KY, KX, srcW, dstW;
+    uint32_t cy[16];             // (c, c) u16 pairs
+    uint32_t cx[8];              // (c_2p, c_2p+1) u16 pairs
+};
+hipError_t launch_area_int(const AreaDev &a, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
+
+// --- exact 2x bilinear upsampler.
+struct LinearDev {
+    int srcW, srcH, dstW, dstH;
+    uint32_t cy[2];              // per phase (c0, c1) u16 pairs
+    uint32_t cx[2];
+};
+hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
+
+} // namespace iqo_amd

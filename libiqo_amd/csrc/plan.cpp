@@ -1,0 +1,580 @@
+// plan.cpp -- host plan construction (see plan.hpp).  Floating-point evaluation follows the
+// reference's types and operation order exactly (double windowed sinc, float sums and float
+// quantisation), compiled without fast-math so the quantised tables are reproducible.
+#include "plan.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
+namespace iqo_amd {
+namespace {
+
+// ---------------------------------------------------------------- integer helpers (src/math.hpp)
+
+int64_t gcd_ref(int64_t a, int64_t b)  // math.hpp:37-49 (result sign as the reference's)
+{
+    for (int64_t r = a % b; r != 0; r = a % b) {
+        a = b;
+        b = r;
+    }
+    return b;
+}
+
+int64_t floor_div(int64_t a, int64_t b)  // math.hpp:58-65
+{
+    return ((a ^ b) < 0) ? (a - b + 1) / b : a / b;
+}
+
+// Exact rational stepping of floor(x * dy / dx) -- math.hpp:70-155 (LinearIterator).
+class RationalStep {
+public:
+    RationalStep(int64_t dx, int64_t dy) : dx_(dx), dy_(dy), x_(0), y_(0) {}
+    void seek(int64_t x)  // setX(x), math.hpp:87-91
+    {
+        x_ = (x * dy_) % dx_;
+        y_ = (x * dy_) / dx_;
+    }
+    void seek_rational(int64_t nume, int64_t deno)  // setX(nume, deno), math.hpp:96-112
+    {
+        y_ = floor_div(nume * dy_, deno * dx_);
+        int64_t n = nume * dx_, ndy = dy_ * deno, ndx = dx_ * deno;
+        int64_t g = std::llabs(gcd_ref(n, gcd_ref(ndy, ndx)));
+        n /= g;
+        ndy /= g;
+        ndx /= g;
+        x_ = n % ndx;
+        if (x_ < 0)
+            x_ += ndx;
+        dx_ = ndx;
+        dy_ = ndy;
+    }
+    void step(int64_t a)  // advance(a), math.hpp:142-149
+    {
+        x_ += a * dy_;
+        while (x_ >= dx_) {
+            ++y_;
+            x_ -= dx_;
+        }
+    }
+    int64_t next()  // *it++
+    {
+        int64_t v = y_;
+        step(1);
+        return v;
+    }
+
+private:
+    int64_t dx_, dy_, x_, y_;
+};
+
+size_t first_max(const std::vector<float> &v)  // std::max_element: first of equal maxima
+{
+    size_t k = 0;
+    for (size_t i = 1; i < v.size(); ++i)
+        if (v[k] < v[i])
+            k = i;
+    return k;
+}
+
+// Quantise so the taps sum exactly to `bias`, +-1 fix-ups at the current float maximum,
+// zeroing it each time.  Lanczos :341-367 (int16) and Area :222-248 (u16) share this scheme.
+template <typename Q>
+void quantise(std::vector<float> f, float sum, int bias, int32_t *out)
+{
+    const size_t n = f.size();
+    int total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        float scaled = f[i] * static_cast<float>(bias) / sum;
+        // iqo::round<float> (math.hpp:12-16), then the narrowing the reference's x86-64 build
+        // performs: truncate to int32, keep the low 16 bits (explicit, so it is not UB here).
+        Q q = static_cast<Q>(static_cast<int32_t>(std::floor(scaled + 0.5f)));
+        out[i] = q;
+        total += q;
+    }
+    for (; total < bias; ++total) {
+        size_t k = first_max(f);
+        out[k] = static_cast<Q>(out[k] + 1);
+        f[k] = 0;
+    }
+    for (; total > bias; --total) {
+        size_t k = first_max(f);
+        out[k] = static_cast<Q>(out[k] - 1);
+        f[k] = 0;
+    }
+}
+
+// ---------------------------------------------------------------- Lanczos window
+
+double lanczos_weight(int degree, double x)  // IQOLanczosResizerImpl_Generic.cpp:10-29
+{
+    const double pi = 3.14159265358979;
+    double ax = std::fabs(x);
+    if (std::fmod(ax, 1.0) < 1e-5)
+        return ax < 1e-5 ? 1.0 : 0.0;
+    if (static_cast<double>(degree) <= ax)
+        return 0.0;
+    double px = pi * x, pxa = pi * (x / degree);
+    return (std::sin(px) / px) * (std::sin(pxa) / pxa);
+}
+
+// calcNumCoefsForLanczos, :32-96
+int lanczos_taps(int degree, size_t rs, size_t rd, size_t pxScale)
+{
+    if (rs <= rd)
+        return 2 * degree;
+    size_t d2 = std::max<size_t>(1, static_cast<size_t>(degree) / pxScale);
+    return static_cast<int>(2 * static_cast<ptrdiff_t>(std::ceil(static_cast<double>(d2 * rs) / static_cast<double>(rd))));
+}
+
+// setLanczosTable, :111-191 -- returns float sum; fills f[taps]
+float lanczos_phase(int degree, size_t rs, size_t rd, ptrdiff_t phase, size_t px, std::vector<float> &f)
+{
+    double begin;
+    if (rs > rd) {
+        int degFactor = std::max(1, static_cast<int>(px) / degree);
+        size_t r = static_cast<size_t>(phase) * rs % rd;
+        begin = static_cast<double>(-degree * degFactor) - 0.5 * static_cast<double>(px) +
+                0.5 * static_cast<double>(rd) * static_cast<double>(px) / static_cast<double>(rs) +
+                static_cast<double>((rd - r) * px % rs) / static_cast<double>(rs);
+    } else {
+        double off = std::fmod(static_cast<double>(static_cast<size_t>(phase) * rs) / static_cast<double>(rd), 1.0);
+        begin = -degree + 1.0 - off;
+        rs = rd;
+        px = 1;
+    }
+    float sum = 0;
+    for (size_t i = 0; i < f.size(); ++i) {
+        double x = begin + static_cast<double>(i * rd * px) / static_cast<double>(rs);
+        f[i] = static_cast<float>(lanczos_weight(degree, x));
+        sum += f[i];
+    }
+    return sum;
+}
+
+// ---------------------------------------------------------------- Area boxes
+
+int area_taps(size_t rs, size_t rd)  // calcNumCoefsForArea, IQOAreaResizerImpl_Generic.cpp:11-65
+{
+    if (rs < rd)
+        return 1;
+    size_t whole = (rs / rd) * rd;
+    size_t n = (rs + rd - 1) / rd;
+    int64_t g = gcd_ref(static_cast<int64_t>(rs), static_cast<int64_t>(whole));
+    int64_t l = static_cast<int64_t>(rs) / g * static_cast<int64_t>(whole);
+    if (l > static_cast<int64_t>(rs))
+        ++n;
+    return static_cast<int>(n);
+}
+
+float area_phase(size_t rs, size_t rd, ptrdiff_t phase, std::vector<float> &f)  // setAreaTable :74-97
+{
+    double b = static_cast<double>(static_cast<size_t>(phase) * rs) / static_cast<double>(rd);
+    double e = static_cast<double>(static_cast<size_t>(phase + 1) * rs) / static_cast<double>(rd);
+    float sum = 0;
+    for (size_t i = 0; i < f.size(); ++i) {
+        double nx = std::min(e, std::floor(b) + 1.0);
+        f[i] = static_cast<float>(nx - b);
+        sum += f[i];
+        b = nx;
+    }
+    return sum;
+}
+
+// ---------------------------------------------------------------- axis builders
+
+struct Reduced {
+    size_t rs, rd;
+};
+
+Reduced reduce(size_t s, size_t d)
+{
+    size_t g = static_cast<size_t>(gcd_ref(static_cast<int64_t>(s), static_cast<int64_t>(d)));
+    return Reduced{s / g, d / g};
+}
+
+void tables_lanczos(unsigned degree, size_t s, size_t d, size_t px, int bias, AxisPlan *a)
+{
+    Reduced r = reduce(s, d);
+    a->taps = lanczos_taps(static_cast<int>(degree), r.rs, r.rd, px);
+    a->phases = static_cast<int>(r.rd);
+    a->table.assign(static_cast<size_t>(a->taps) * a->phases, 0);
+    std::vector<float> f(static_cast<size_t>(a->taps));
+    for (int q = 0; q < a->phases; ++q) {
+        float sum = lanczos_phase(static_cast<int>(degree), r.rs, r.rd, q, px, f);
+        quantise<int16_t>(f, sum, bias, &a->table[static_cast<size_t>(q) * a->taps]);
+    }
+}
+
+void tables_area(size_t s, size_t d, int bias, AxisPlan *a)
+{
+    Reduced r = reduce(s, d);
+    a->taps = area_taps(r.rs, r.rd);
+    a->phases = static_cast<int>(r.rd);
+    a->table.assign(static_cast<size_t>(a->taps) * a->phases, 0);
+    std::vector<float> f(static_cast<size_t>(a->taps));
+    for (int q = 0; q < a->phases; ++q) {
+        float sum = area_phase(r.rs, r.rd, q, f);
+        quantise<uint16_t>(f, sum, bias, &a->table[static_cast<size_t>(q) * a->taps]);
+    }
+}
+
+// setLinearTable + adjustCoefs, IQOLinearResizerImpl_Generic.cpp:29-69, 193-208
+void tables_linear(size_t s, size_t d, int bias, AxisPlan *a)
+{
+    Reduced r = reduce(s, d);
+    a->taps = 2;
+    a->phases = static_cast<int>(r.rd);
+    a->table.assign(2 * static_cast<size_t>(a->phases), 0);
+    for (size_t i = 0; i < r.rd; ++i) {
+        double ip;
+        double x = static_cast<double>(i);
+        float c1 = static_cast<float>(std::modf((x + 0.5) * static_cast<double>(r.rs) / static_cast<double>(r.rd) + 0.5, &ip));
+        float c0 = 1.0f - c1;
+        uint16_t q0 = static_cast<uint16_t>(static_cast<int32_t>(std::floor(c0 * static_cast<float>(bias) + 0.5f)));
+        a->table[2 * i] = q0;
+        a->table[2 * i + 1] = static_cast<uint16_t>(bias - q0);
+    }
+}
+
+int clampi(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Lanczos Y map: simulate the three row loops with their SHARED iterator and table cursor
+// (:390-453); a later loop overwrites rows an earlier one wrote when mainEnd < mainBegin.
+void coords_lanczos_y(AxisPlan *a)
+{
+    const int64_t s = a->srcLen, d = a->dstLen, m = a->taps / 2;
+    a->coord.assign(static_cast<size_t>(d), CoordInfo{0, 0, kMain, 0});
+    if (s == d) {
+        a->identity = true;
+        for (int64_t y = 0; y < d; ++y)
+            a->coord[y] = CoordInfo{static_cast<int32_t>(y), 0, kIdentity, 0};
+        return;
+    }
+    int64_t mb = ((m - 1) * d + s - 1) / s;
+    int64_t me = std::max<int64_t>(0, (s - m) * d / s);
+    a->mainBegin = static_cast<int>(mb);
+    a->mainEnd = static_cast<int>(me);
+    RationalStep it(d, s);
+    int64_t cursor = 0;
+    auto emit = [&](int64_t y, int32_t kind) {
+        int64_t o = it.next() + 1;
+        CoordInfo c{static_cast<int32_t>(o - m), static_cast<int32_t>(cursor), kind, 0};
+        cursor += a->taps;
+        if (cursor == static_cast<int64_t>(a->taps) * a->phases)
+            cursor = 0;
+        if (kind != kMain) {
+            int16_t den = 0;  // wrapped int16 sum over valid rows (resizeYborder :477-485)
+            for (int i = 0; i < a->taps; ++i) {
+                int64_t r = c.srcO + i;
+                if (r >= 0 && r < s)
+                    den = static_cast<int16_t>(den + a->table[c.tabOff + i]);
+            }
+            c.aux = den;
+        }
+        a->coord[static_cast<size_t>(y)] = c;
+    };
+    for (int64_t y = 0; y < mb; ++y)
+        emit(y, kBorderLo);
+    for (int64_t y = mb; y < me; ++y)
+        emit(y, kMain);
+    for (int64_t y = me; y < d; ++y)
+        emit(y, kBorderHi);
+}
+
+// Lanczos X map (resizeX / resizeXborder / resizeXmain, :518-612): each column is independent.
+void coords_lanczos_x(AxisPlan *a)
+{
+    const int64_t s = a->srcLen, d = a->dstLen, m = a->taps / 2;
+    a->coord.assign(static_cast<size_t>(d), CoordInfo{0, 0, kMain, 0});
+    if (s == d) {
+        a->identity = true;
+        for (int64_t x = 0; x < d; ++x)
+            a->coord[x] = CoordInfo{static_cast<int32_t>(x), 0, kIdentity, 0};
+        return;
+    }
+    int64_t mb = ((m - 1) * d + s - 1) / s;
+    int64_t me = std::max<int64_t>(0, (s - m) * d / s);
+    a->mainBegin = static_cast<int>(mb);
+    a->mainEnd = static_cast<int>(me);
+    for (int64_t x = 0; x < d; ++x) {
+        CoordInfo c;
+        c.srcO = static_cast<int32_t>(x * s / d + 1 - m);
+        c.tabOff = static_cast<int32_t>((x % a->phases) * a->taps);
+        c.kind = (x >= me) ? kBorderHi : (x < mb ? kBorderLo : kMain);
+        c.aux = 0;
+        if (c.kind != kMain) {
+            int32_t den = 0;  // int32 sum over valid columns (resizeXborder :563-570)
+            for (int i = 0; i < a->taps; ++i) {
+                int64_t col = c.srcO + i;
+                if (col >= 0 && col < s)
+                    den += a->table[c.tabOff + i];
+            }
+            c.aux = den;
+        }
+        a->coord[static_cast<size_t>(x)] = c;
+    }
+}
+
+// Area map: o = floor(i*s/d), phase i mod rd (IQOAreaResizerImpl_Generic.cpp:271-293, 340-368)
+void coords_area(AxisPlan *a)
+{
+    const int64_t s = a->srcLen, d = a->dstLen;
+    a->coord.resize(static_cast<size_t>(d));
+    a->identity = (s == d);
+    a->mainBegin = 0;
+    a->mainEnd = static_cast<int>(d);
+    for (int64_t i = 0; i < d; ++i) {
+        if (a->identity)
+            a->coord[i] = CoordInfo{static_cast<int32_t>(i), 0, kIdentity, 0};
+        else
+            a->coord[i] = CoordInfo{static_cast<int32_t>(i * s / d), static_cast<int32_t>((i % a->phases) * a->taps), kMain, 0};
+    }
+}
+
+// Linear map (IQOLinearResizerImpl_Generic.cpp:210-282, 327-407): border width from
+// convertCoordinate(srcLen, dstLen, 0) (always 1, :13-22); interior origin from
+// LinearIterator(d, s).setX(s - d, 2d) advanced to mainBegin.
+void coords_linear(AxisPlan *a)
+{
+    const int64_t s = a->srcLen, d = a->dstLen;
+    a->coord.resize(static_cast<size_t>(d));
+    if (s == d) {
+        a->identity = true;
+        for (int64_t i = 0; i < d; ++i)
+            a->coord[i] = CoordInfo{static_cast<int32_t>(i), 0, kIdentity, 0};
+        return;
+    }
+    double toX = (0.5 + static_cast<double>(s)) * 0.0 / static_cast<double>(d) - 0.5;
+    int mb0 = static_cast<int>(std::ceil(std::fabs(toX)));
+    int mb = clampi(0, static_cast<int>(d), mb0);
+    int me = clampi(0, static_cast<int>(d), static_cast<int>(d) - mb);
+    a->mainBegin = mb;
+    a->mainEnd = me;
+    RationalStep it(d, s);
+    it.seek_rational(s - d, 2 * d);
+    it.step(mb);
+    for (int64_t i = 0; i < d; ++i) {
+        if (i >= me)
+            a->coord[i] = CoordInfo{static_cast<int32_t>(s - 1), 0, kBorderHi, 0};
+        else if (i < mb)
+            a->coord[i] = CoordInfo{0, 0, kBorderLo, 0};
+        else
+            a->coord[i] = CoordInfo{static_cast<int32_t>(it.next()), static_cast<int32_t>((i % a->phases) * 2), kMain, 0};
+    }
+}
+
+// ---------------------------------------------------------------- fast-path eligibility
+
+void pick_fast_lanczos(Plan *p)
+{
+    AxisPlan &x = p->x, &y = p->y;
+    if (x.identity || y.identity || x.phases != 1 || y.phases != 1)
+        return;
+    if (p->srcW % p->dstW || p->srcH % p->dstH)
+        return;
+    int KX = p->srcW / p->dstW, KY = p->srcH / p->dstH;
+    if (x.mainBegin > x.mainEnd || y.mainBegin > y.mainEnd)
+        return;
+    if (y.mainBegin > 16 || p->dstH - y.mainEnd > 16 || x.mainBegin > 16 || p->dstW - x.mainEnd > 16)
+        return;
+    FastLanczos &f = p->flz;
+    f.KY = KY;
+    f.KX = KX;
+    // Y: drop zero taps at both ends (exact for main and masked formulas alike).
+    int m = y.taps / 2, lo = 0, hi = y.taps;
+    while (lo < hi && y.table[lo] == 0)
+        ++lo;
+    while (hi > lo && y.table[hi - 1] == 0)
+        --hi;
+    f.NY = hi - lo;
+    f.offY = 1 - m + lo;  // first tap row = KY*y + 1 - m + lo  (srcOY = floor(y*KY) + 1)
+    f.cy.assign(y.table.begin() + lo, y.table.begin() + hi);
+    // X: drop zero taps, then pad to an even first column and an even tap count (int16 pairs).
+    int mx = x.taps / 2, xl = 0, xh = x.taps;
+    while (xl < xh && x.table[xl] == 0)
+        ++xl;
+    while (xh > xl && x.table[xh - 1] == 0)
+        --xh;
+    int off = 1 - mx + xl;  // first tap column = KX*x + off
+    int pre = (((KX % 2) == 0) && (off & 1)) ? 1 : 0;
+    if (KX % 2)
+        return;  // odd KX alternates pair parity per output: not instantiated
+    f.offX = off - pre;
+    int n = (xh - xl) + pre;
+    f.NXP = n + (n & 1);
+    f.cx.assign(static_cast<size_t>(f.NXP), 0);
+    for (int i = xl; i < xh; ++i)
+        f.cx[static_cast<size_t>(i - xl + pre)] = static_cast<int16_t>(x.table[i]);
+    f.mainBeginY = y.mainBegin;
+    f.mainEndY = y.mainEnd;
+    f.mainBeginX = x.mainBegin;
+    f.mainEndX = x.mainEnd;
+    f.denoYTop.clear();
+    f.denoYBot.clear();
+    for (int r = 0; r < y.mainBegin; ++r)
+        f.denoYTop.push_back(y.coord[r].aux);
+    for (int r = y.mainEnd; r < p->dstH; ++r)
+        f.denoYBot.push_back(y.coord[r].aux);
+    f.dXLeft.clear();
+    f.dXRight.clear();
+    for (int c = 0; c < x.mainBegin; ++c)
+        f.dXLeft.push_back(64 * x.coord[c].aux);
+    for (int c = x.mainEnd; c < p->dstW; ++c)
+        f.dXRight.push_back(64 * x.coord[c].aux);
+    // instantiated shapes (kernels.hip): (KY,KX,NY,NXP,offX/2) = (2,2,10,14,-3) Lanczos-3 2:1,
+    // (2,2,8,10,-2) Lanczos-2 2:1.  Everything else runs the general kernel.
+    bool inst = KY == 2 && KX == 2 && ((f.NY == 10 && f.NXP == 14 && f.offX == -6) ||
+                                       (f.NY == 8 && f.NXP == 10 && f.offX == -4));
+    if (!inst || (p->srcW % 16) || p->srcW > 8192)
+        return;
+    p->kernel = 1;  // IQO_KERNEL_LANCZOS_STREAM
+}
+
+void pick_fast_area(Plan *p)
+{
+    AxisPlan &x = p->x, &y = p->y;
+    if (x.identity || y.identity || x.phases != 1 || y.phases != 1)
+        return;
+    if (p->srcW % p->dstW || p->srcH % p->dstH)
+        return;
+    int KX = p->srcW / p->dstW, KY = p->srcH / p->dstH;
+    if (!(KX == 2 || KX == 4 || KX == 8) || KY < 2 || KY > 16 || x.taps != KX || y.taps != KY)
+        return;
+    if (p->srcW % 32)
+        return;
+    p->far.KX = KX;
+    p->far.KY = KY;
+    p->far.cx.assign(x.table.begin(), x.table.end());
+    p->far.cy.assign(y.table.begin(), y.table.end());
+    p->kernel = 2;  // IQO_KERNEL_AREA_INT
+}
+
+void pick_fast_linear(Plan *p)
+{
+    AxisPlan &x = p->x, &y = p->y;
+    if (x.identity || y.identity || p->dstW != 2 * p->srcW || p->dstH != 2 * p->srcH)
+        return;
+    if (x.phases != 2 || y.phases != 2 || p->dstW % 16)
+        return;
+    for (const AxisPlan *a : {&x, &y}) {
+        if (a->mainBegin != 1 || a->mainEnd != a->dstLen - 1)
+            return;
+        for (int i = a->mainBegin; i < a->mainEnd; ++i)
+            if (a->coord[i].srcO != ((i - 1) >> 1) || a->coord[i].tabOff != (i % 2) * 2)
+                return;
+    }
+    for (int q = 0; q < 2; ++q)
+        for (int k = 0; k < 2; ++k) {
+            p->fln.cx[q][k] = static_cast<uint16_t>(x.table[2 * q + k]);
+            p->fln.cy[q][k] = static_cast<uint16_t>(y.table[2 * q + k]);
+        }
+    p->kernel = 3;  // IQO_KERNEL_LINEAR_UP2
+}
+
+} // namespace
+
+bool build_tables(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                  size_t pxScale, AxisPlan *x, AxisPlan *y, std::string *err)
+{
+    if (!srcW || !srcH || !dstW || !dstH) {
+        if (err)
+            *err = "zero-sized image";
+        return false;
+    }
+    if (srcW > (1u << 30) || srcH > (1u << 30) || dstW > (1u << 30) || dstH > (1u << 30)) {
+        if (err)
+            *err = "image dimension too large";
+        return false;
+    }
+    x->srcLen = static_cast<int>(srcW);
+    x->dstLen = static_cast<int>(dstW);
+    y->srcLen = static_cast<int>(srcH);
+    y->dstLen = static_cast<int>(dstH);
+    switch (m) {
+    case kLanczos:
+        if (degree < 1 || pxScale < 1) {
+            if (err)
+                *err = "lanczos degree and pxScale must be >= 1";
+            return false;
+        }
+        tables_lanczos(degree, srcW, dstW, pxScale, 1 << 14, x);  // kBias14 (:265-266)
+        tables_lanczos(degree, srcH, dstH, pxScale, 1 << 6, y);   // kBias   (:262-263)
+        return true;
+    case kArea:
+        tables_area(srcW, dstW, 1 << 15, x);  // kBias15 (IQOAreaResizerImpl_Generic.cpp:148-149)
+        tables_area(srcH, dstH, 1 << 8, y);   // kBias   (:145-146)
+        return true;
+    case kLinear:
+        tables_linear(srcW, dstW, 1 << 15, x);  // IQOLinearResizerImpl_Generic.cpp:135-136
+        tables_linear(srcH, dstH, 1 << 8, y);
+        return true;
+    }
+    if (err)
+        *err = "unknown method";
+    return false;
+}
+
+bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                size_t pxScale, Plan *p, std::string *err)
+{
+    *p = Plan();
+    if (!build_tables(m, degree, srcW, srcH, dstW, dstH, pxScale, &p->x, &p->y, err))
+        return false;
+    p->method = m;
+    p->degree = degree;
+    p->pxScale = pxScale;
+    p->srcW = static_cast<int>(srcW);
+    p->srcH = static_cast<int>(srcH);
+    p->dstW = static_cast<int>(dstW);
+    p->dstH = static_cast<int>(dstH);
+    switch (m) {
+    case kLanczos:
+        coords_lanczos_x(&p->x);
+        coords_lanczos_y(&p->y);
+        pick_fast_lanczos(p);
+        break;
+    case kArea:
+        coords_area(&p->x);
+        coords_area(&p->y);
+        pick_fast_area(p);
+        break;
+    case kLinear:
+        coords_linear(&p->x);
+        coords_linear(&p->y);
+        pick_fast_linear(p);
+        break;
+    }
+    return true;
+}
+
+void band_src_rows(const Plan &p, int r0, int r1, int *s0, int *s1)
+{
+    int lo = p.srcH, hi = 0;
+    for (int yy = r0; yy < r1; ++yy) {
+        const CoordInfo &c = p.y.coord[static_cast<size_t>(yy)];
+        int a, b;  // [a, b) rows touched
+        if (c.kind == kIdentity) {
+            a = c.srcO;
+            b = c.srcO + 1;
+        } else if (p.method == kLinear && c.kind != kMain) {
+            a = c.kind == kBorderLo ? 0 : p.srcH - 1;
+            b = a + 1;
+        } else {
+            a = c.srcO;
+            b = c.srcO + p.y.taps;
+        }
+        a = std::max(0, std::min(a, p.srcH - 1));
+        b = std::max(a + 1, std::min(b, p.srcH));
+        lo = std::min(lo, a);
+        hi = std::max(hi, b);
+    }
+    if (lo >= hi) {
+        lo = 0;
+        hi = 0;
+    }
+    *s0 = lo;
+    *s1 = hi;
+}
+
+} // namespace iqo_amd

@@ -1,0 +1,95 @@
+// plan.hpp -- host-side resize plan: quantised coefficient tables, per-row / per-column index
+// maps and the fast-path decision.  Pure C++ (no HIP), built once per resizer and uploaded.
+//
+// The tables restate the reference's init() (table construction is host work there too):
+//   Lanczos  src/IQOLanczosResizerImpl_Generic.cpp:32-191, 291-367
+//   Area     src/IQOAreaResizerImpl_Generic.cpp:11-97, 174-248
+//   Linear   src/IQOLinearResizerImpl_Generic.cpp:13-69, 157-208
+// and the index maps restate the row/column drivers (resize / resizeX) so that every output
+// coordinate carries (first source index, table phase, formula kind) exactly as the reference
+// computes it -- including the shared-iterator behaviour of the Lanczos row loops
+// (IQOLanczosResizerImpl_Generic.cpp:390-453) on images too small for a main region.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace iqo_amd {
+
+enum Method { kLanczos = 0, kArea = 1, kLinear = 2 };
+
+// Formula applied at one output coordinate of one axis.
+enum Kind : int32_t {
+    kMain = 0,      // interior formula (no masking)
+    kBorderLo = 1,  // Lanczos: masked + renormalised; Linear: replicate first source px/row
+    kBorderHi = 2,  // Lanczos: masked + renormalised; Linear: replicate last source px/row
+    kIdentity = 3   // srcLen == dstLen shortcut of the reference (resize():378, resizeX():520)
+};
+
+// Per output coordinate record, uploaded as int4 {srcO, tabOff, kind, aux}.
+struct CoordInfo {
+    int32_t srcO;    // source index of tap 0 (may be < 0 or >= srcLen at Lanczos borders)
+    int32_t tabOff;  // phase * taps (offset into the axis table)
+    int32_t kind;    // Kind
+    int32_t aux;     // Lanczos border denominator: Y = wrapped int16 sum of valid taps,
+                     // X = int32 sum of valid taps; unused otherwise
+};
+
+struct AxisPlan {
+    int srcLen = 0, dstLen = 0;
+    int taps = 0, phases = 0;     // table geometry (reference m_NumCoefs*, m_NumTables*)
+    std::vector<int32_t> table;   // phases * taps; int16 (Lanczos) or u16 (Area/Linear) values
+    bool identity = false;
+    int mainBegin = 0, mainEnd = 0;
+    std::vector<CoordInfo> coord; // dstLen records
+};
+
+// Parameters of the fast kernels (IQO_KERNEL_* != GENERAL), filled when eligible.
+struct FastLanczos {
+    int KY = 0, KX = 0;           // integer decimation factors
+    int NY = 0;                   // Y taps after trimming zero coefficients
+    int offY = 0;                 // first tap row = KY*y + offY
+    int NXP = 0;                  // X taps after trimming + padding to even start and even count
+    int offX = 0;                 // first (padded) tap column = KX*x + offX (even)
+    std::vector<int16_t> cy;      // NY
+    std::vector<int16_t> cx;      // NXP (zero padded)
+    int mainBeginY = 0, mainEndY = 0, mainBeginX = 0, mainEndX = 0;
+    std::vector<int32_t> denoYTop, denoYBot; // wrapped int16 valid-tap sums per border row
+    std::vector<int32_t> dXLeft, dXRight;    // 64 * valid-tap sum per border column
+};
+
+struct FastArea {
+    int KY = 0, KX = 0;
+    std::vector<uint16_t> cy, cx;
+};
+
+struct FastLinear {
+    uint16_t cy[2][2] = {{0, 0}, {0, 0}}, cx[2][2] = {{0, 0}, {0, 0}};
+};
+
+struct Plan {
+    Method method = kLanczos;
+    unsigned degree = 0;
+    size_t pxScale = 1;
+    int srcW = 0, srcH = 0, dstW = 0, dstH = 0;
+    AxisPlan x, y;
+    int kernel = 0;               // IQO_KERNEL_* for aligned full-frame calls
+    FastLanczos flz;
+    FastArea far;
+    FastLinear fln;
+};
+
+// Build the full plan.  Returns false (with *err) for invalid arguments.
+bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                size_t pxScale, Plan *out, std::string *err);
+
+// Tables only (cheap; used by the host-only ABI query).
+bool build_tables(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                  size_t pxScale, AxisPlan *x, AxisPlan *y, std::string *err);
+
+// Source rows read by output rows [r0, r1) (global indices; clamped to [0, srcH)).
+void band_src_rows(const Plan &p, int r0, int r1, int *s0, int *s1);
+
+} // namespace iqo_amd

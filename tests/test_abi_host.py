@@ -1,0 +1,108 @@
+"""Boundary + host logic, no GPU: the C-ABI library loads, exports every symbol include/*.h
+declares, and the product's host plan (table builder, libiqo_amd/csrc/plan.cpp) reproduces the
+reference's quantised tables from tests/golden bit for bit."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import libiqo_amd
+import oracle_lib as ol
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions(header):
+    text = open(header).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(iqo_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = libiqo_amd.lib()
+    names = _declared_functions(os.path.join(ROOT, "include", "iqo_hip.h"))
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(lib, n), n
+    out = subprocess.run(["nm", "-D", "--defined-only", libiqo_amd.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(r"\bT %s\b" % n, out), n
+
+
+def test_library_exports_dropin_cpp_classes():
+    out = subprocess.run(["nm", "-DC", "--defined-only", libiqo_amd.LIB_PATH], capture_output=True, text=True).stdout
+    for sym in ["iqo::LanczosResizer::LanczosResizer(unsigned int, unsigned long, unsigned long, unsigned long, unsigned long, unsigned long)",
+                "iqo::LanczosResizer::resize(unsigned long, unsigned char const*, unsigned long, unsigned char*)",
+                "iqo::AreaResizer::AreaResizer(unsigned long, unsigned long, unsigned long, unsigned long)",
+                "iqo::AreaResizer::resize(unsigned long, unsigned char const*, unsigned long, unsigned char*)",
+                "iqo::LinearResizer::LinearResizer(unsigned long, unsigned long, unsigned long, unsigned long)",
+                "iqo::LinearResizer::resize(unsigned long, unsigned char const*, unsigned long, unsigned char*)",
+                "iqo::LanczosResizer::~LanczosResizer()"]:
+        assert sym in out, sym
+
+
+def test_version_and_errors():
+    lib = libiqo_amd.lib()
+    assert b"gfx950" in lib.iqo_hip_version()
+    assert lib.iqo_hip_strerror(-1) == b"invalid argument"
+    p = ctypes.c_void_p()
+    assert lib.iqo_hip_plan_lanczos(3, 0, 10, 5, 5, 1, 0, ctypes.byref(p)) != 0
+    assert not p.value
+
+
+def test_no_gpu_means_no_plan():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except ImportError:
+        pass
+    assert libiqo_amd.available() == 0
+    with pytest.raises(libiqo_amd.IqoError):
+        libiqo_amd.LanczosResizer(3, 64, 48, 32, 24)
+
+
+def test_host_tables_match_reference_golden(golden):
+    n = 0
+    for c in golden["cases"]:
+        for axis, name in ((0, "tableX"), (1, "tableY")):
+            # the product builds tables strict-IEEE, like the reference without -Ofast
+            key = name if c[name + "_ofast_strict_agree"] else name + "_strict"
+            if key not in c:
+                continue
+            rows = libiqo_amd.host_tables(c["method"], c["degree"], c["srcW"], c["srcH"], c["dstW"], c["dstH"],
+                                          c["pxScale"], axis)
+            assert [len(rows), len(rows[0])] == c[name + "_shape"], c["id"]
+            assert sum(rows, []) == c[key], (c["id"], name)
+            n += 1
+    assert n > 800
+
+
+def test_host_tables_match_oracle_random():
+    import random
+    rng = random.Random(7)
+    for _ in range(300):
+        m = rng.choice(["lanczos", "area", "linear"])
+        d = rng.randint(1, 9)
+        px = rng.choice([1, 2, 3])
+        sw, sh = rng.randint(1, 3000), rng.randint(1, 3000)
+        dw, dh = rng.randint(1, 3000), rng.randint(1, 3000)
+        for axis in (0, 1):
+            a = libiqo_amd.host_tables(m, d, sw, sh, dw, dh, px, axis)
+            b = ol.oracle_tables(m, d, sw, sh, dw, dh, px, axis).tolist()
+            assert a == b, (m, d, sw, sh, dw, dh, px, axis)
+
+
+@pytest.mark.parametrize("cfg,kernel", [
+    (("lanczos", 3, 3840, 2160, 1920, 1080, 1), "lanczos_stream"),
+    (("lanczos", 2, 640, 480, 320, 240, 1), "lanczos_stream"),
+    (("area", 0, 7680, 4320, 1920, 1080, 1), "area_int"),
+    (("linear", 0, 1920, 1080, 3840, 2160, 1), "linear_up2"),
+    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "general"),
+    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "general"),
+    (("area", 0, 1920, 1080, 1280, 720, 1), "general"),
+])
+def test_fast_path_selection(cfg, kernel):
+    assert libiqo_amd.host_kernel_for(*cfg) == kernel
