@@ -88,6 +88,16 @@ __device__ __forceinline__ int exact_div(int n, int d)
 
 __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 
+// A value the instruction combiner cannot see through.  Used on clamped bytes before packing:
+// ROCm 7.2 otherwise folds (sat_u8(a >> n), sat_u8(b >> n)) into gfx950's v_ashr_pk_u8_i32 and
+// then ORs further bytes into bits 16..31 of its result as if they were zero, which corrupted
+// bytes 2-3 of every packed word on the GPU (caught by tests/test_gpu_parity.py).
+__device__ __forceinline__ uint32_t opaque(uint32_t v)
+{
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
 // Compile-time loop: f(std::integral_constant<int, 0>) ... f(integral_constant<int, N-1>), so
 // register-array indices derived from the induction variable are constants (no scratch).
 template <typename F, int... I>
@@ -318,21 +328,23 @@ __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
                         s = pk_mad(win[(u * KY + i) % NY][c], L.cy[i], s);
                     acc[c] = s;
                 }
-                if (yy < L.mainBeginY || yy >= L.mainEndY) {
-                    // border row: work = int16(int(nume) * 64 / deno)   (resizeYborder :487-489)
-                    const int den = yy < L.mainBeginY ? L.border[yy] : L.border[16 + yy - L.mainEndY];
-#pragma unroll
-                    for (int c = 0; c < 8; ++c) {
-                        int lo = static_cast<int16_t>(acc[c] & 0xffffu), hi = static_cast<int16_t>(acc[c] >> 16);
-                        lo = static_cast<uint16_t>(static_cast<int16_t>(exact_div(lo * 64, den)));
-                        hi = static_cast<uint16_t>(static_cast<int16_t>(exact_div(hi * 64, den)));
-                        acc[c] = static_cast<uint32_t>(lo) | (static_cast<uint32_t>(hi) << 16);
-                    }
-                }
                 uint32_t *row = lds + (yy & 1) * BS + kPadW;
                 if (active) {
                     *reinterpret_cast<uint4 *>(row + 8 * t) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
                     *reinterpret_cast<uint4 *>(row + 8 * t + 4) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+                    if (yy < L.mainBeginY || yy >= L.mainEndY) {
+                        // border row (uniform, rare): work = int16(int(nume) * 64 / deno), resizeYborder
+                        // :487-489.  Compact loop over this thread's own 16 LDS values.
+                        const int den = yy < L.mainBeginY ? L.border[yy] : L.border[16 + yy - L.mainEndY];
+                        uint32_t *w32 = row + 8 * t;
+#pragma unroll 1
+                        for (int c = 0; c < 8; ++c) {
+                            const uint32_t v = w32[c];
+                            const int lo = exact_div(static_cast<int>(static_cast<int16_t>(v & 0xffffu)) * 64, den);
+                            const int hi = exact_div(static_cast<int>(static_cast<int16_t>(v >> 16)) * 64, den);
+                            w32[c] = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
+                        }
+                    }
                 }
                 __syncthreads();
                 // ---- horizontal taps from LDS (int16 pairs . coefficient pairs -> int32)
@@ -346,30 +358,58 @@ __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
                     d[4 * r + 2] = q.z;
                     d[4 * r + 3] = q.w;
                 }
-                int sum[OUTS];
+                uint32_t ow[OUTS / 4];
 #pragma unroll
-                for (int k = 0; k < OUTS; ++k) {
-                    int s = 1 << 19;
+                for (int k4 = 0; k4 < OUTS / 4; ++k4) {
+                    uint32_t word = 0;
 #pragma unroll
-                    for (int p = 0; p < NXP / 2; ++p)
-                        s = sdot2(d[(KX * k) / 2 + OFFXD - D0 + p], L.cx[p], s);
-                    sum[k] = s >> 20;
-                    const int x = OUTS * t + k;
-                    if (x < L.mainBeginX)  // border column: int16((nume + 2^19) / (deno * 64))
-                        sum[k] = exact_div(s, L.border[32 + x]);
-                    else if (x >= L.mainEndX)
-                        sum[k] = exact_div(s, L.border[48 + x - L.mainEndX]);
-                    sum[k] = clamp255(static_cast<int16_t>(sum[k]));
+                    for (int kk = 0; kk < 4; ++kk) {
+                        const int k = 4 * k4 + kk;
+                        int s = 1 << 19;
+#pragma unroll
+                        for (int p = 0; p < NXP / 2; ++p)
+                            s = sdot2(d[(KX * k) / 2 + OFFXD - D0 + p], L.cx[p], s);
+                        word |= opaque(static_cast<uint32_t>(clamp255(static_cast<int16_t>(s >> 20)))) << (8 * kk);
+                    }
+                    ow[k4] = word;
+                }
+                const int xbase = OUTS * t;
+                if (active && (xbase < L.mainBeginX || xbase + OUTS > L.mainEndX)) {
+                    // border columns (edge threads only): int16((nume + 2^19) / (deno * 64)),
+                    // resizeXborder :572 -- nume is the same dot product (invalid taps read the
+                    // zero pads), only the divisor differs.  Compact, not unrolled.
+                    auto w16 = [&](int c) {  // int16 work value at column c (c may be < 0: zero pad)
+                        const uint32_t v = row[c >> 1];
+                        return static_cast<int>(static_cast<int16_t>((c & 1) ? (v >> 16) : (v & 0xffffu)));
+                    };
+#pragma unroll 1
+                    for (int k = 0; k < OUTS; ++k) {
+                        const int x = xbase + k;
+                        if (x >= L.mainBeginX && x < L.mainEndX)
+                            continue;
+                        const int c0 = KX * x + L.offX;
+                        int s = 1 << 19;
+#pragma unroll 1
+                        for (int p = 0; p < NXP / 2; ++p) {
+                            const uint32_t cc = L.cx[p];
+                            s += w16(c0 + 2 * p) * static_cast<int16_t>(cc & 0xffffu) +
+                                 w16(c0 + 2 * p + 1) * static_cast<int16_t>(cc >> 16);
+                        }
+                        const int dv = x < L.mainBeginX ? L.border[32 + x] : L.border[48 + x - L.mainEndX];
+                        const uint32_t v = static_cast<uint32_t>(clamp255(static_cast<int16_t>(exact_div(s, dv))));
+                        const int sh = 8 * (k & 3);
+#pragma unroll
+                        for (int k4 = 0; k4 < OUTS / 4; ++k4)
+                            if ((k >> 2) == k4)
+                                ow[k4] = (ow[k4] & ~(0xffu << sh)) | (v << sh);
+                    }
                 }
                 if (active) {
                     uint8_t *out = dstF + static_cast<int64_t>(yy - a.io.dstRow0) * a.io.dstSt;
-                    uint32_t w0 = sum[0] | (sum[1] << 8) | (sum[2] << 16) | (sum[3] << 24);
-                    if constexpr (OUTS == 8) {
-                        uint32_t w1 = sum[4] | (sum[5] << 8) | (sum[6] << 16) | (sum[7] << 24);
-                        *reinterpret_cast<uint2 *>(out) = make_uint2(w0, w1);
-                    } else {
-                        *reinterpret_cast<uint32_t *>(out) = w0;
-                    }
+                    if constexpr (OUTS == 8)
+                        *reinterpret_cast<uint2 *>(out) = make_uint2(ow[0], ow[1]);
+                    else
+                        *reinterpret_cast<uint32_t *>(out) = ow[0];
                 }
             }
         });
@@ -419,7 +459,7 @@ __global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
             sum = udot2(acc[(KX * k) / 2 + p], a.g.cx[p], sum);
         int v = static_cast<int16_t>(static_cast<int>(sum) >> 23);
         uint16_t u = static_cast<uint16_t>(v);
-        out[k] = u > 255 ? 255u : u;
+        out[k] = opaque(u > 255 ? 255u : u);
     }
     uint8_t *d = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt +
                  static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt + OUTS * gcol;
@@ -511,7 +551,7 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
             uint32_t pairj = (j == 0) ? W[0] : pair;
             uint32_t sum = udot2(pairj, g.cx[j & 1], 1u << 22);
             uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(sum) >> 23));
-            uint32_t v = u > 255 ? 255u : u;
+            uint32_t v = opaque(u > 255 ? 255u : u);
             word |= v << (8 * jj);
         }
         outw[j4] = word;
