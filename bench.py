@@ -127,6 +127,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--force-general", action="store_true")
+    ap.add_argument("--debug-flags", type=int, default=0, help="timing experiments (wrong output)")
     args = ap.parse_args()
 
     import torch
@@ -154,6 +155,8 @@ def main():
         r.set_option("bands", args.bands)
     if args.force_general:
         r.set_option("force_general", 1)
+    if args.debug_flags:
+        r.set_option("debug_flags", args.debug_flags)
     kernel = r.describe()["kernel"]
 
     gen = torch.Generator(device=dev)

@@ -31,6 +31,7 @@ struct iqo_hip_plan {
     int nChunks = 0, ldsInts = 0;
     bool forceGeneral = false;
     int bands = 0;
+    int debugFlags = 0;
     hipStream_t stream = nullptr;
     uint8_t *stageSrc = nullptr, *stageDst = nullptr;
     size_t stageSrcCap = 0, stageDstCap = 0;
@@ -278,6 +279,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             l.mainBeginX = f.mainBeginX;
             l.mainEndX = f.mainEndX;
             l.border = h->dBorder;
+            l.dbg = h->debugFlags;
             int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
             e = iqo_amd::launch_lanczos_stream(l, io, rb, re, bands, s);
         } else if (kernel == IQO_KERNEL_AREA_INT) {
@@ -389,6 +391,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_EINVAL;
     if (!std::strcmp(key, "force_general")) {
         h->forceGeneral = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "debug_flags")) {  // timing experiments only: results are wrong
+        h->debugFlags = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "bands")) {

@@ -19,6 +19,7 @@ namespace {
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // 16-byte streaming load (source pixels are read once per band): nontemporal hint.
 __device__ __forceinline__ uint4 load16_nt(const uint8_t *p)
@@ -84,6 +85,26 @@ __device__ __forceinline__ int exact_div(int n, int d)
         rem -= ad;
     }
     return ((n ^ d) < 0) ? -static_cast<int>(q) : static_cast<int>(q);
+}
+
+// Fast exact truncating division for the streamer's border paths.  Precondition (holds there):
+// |n| < 2^24 or |d| >= 64, and |n / d| < 2^22 -- then the float estimate is within 1 of the
+// true quotient, and two branch-free correction steps each way make it exact.
+__device__ __forceinline__ int exact_div_fast(int n, int d)
+{
+    const uint32_t an = n < 0 ? 0u - static_cast<uint32_t>(n) : static_cast<uint32_t>(n);
+    const uint32_t ad = d < 0 ? 0u - static_cast<uint32_t>(d) : static_cast<uint32_t>(d);
+    const float r = __builtin_amdgcn_rcpf(static_cast<float>(ad));
+    uint32_t q = static_cast<uint32_t>(static_cast<float>(an) * r);
+    int rem = static_cast<int>(an - q * ad);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const bool lo = rem < 0, hi = rem >= static_cast<int>(ad);
+        q = lo ? q - 1 : (hi ? q + 1 : q);
+        rem = lo ? rem + static_cast<int>(ad) : (hi ? rem - static_cast<int>(ad) : rem);
+    }
+    const int sq = ((n ^ d) < 0) ? -static_cast<int>(q) : static_cast<int>(q);
+    return d == 0 ? 0 : sq;
 }
 
 __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
@@ -248,6 +269,9 @@ struct LanczosArgs {
     LanczosDev l;
     Io io;
     int rowBegin, rowEnd, rowsPerBand;
+    int srcBytes, dstBytes;  // extent of one frame's source window / destination band (buffer range)
+    int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
+                             // 2 = no prefetch loads, 4 = no barrier.  0 in production.
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -258,7 +282,7 @@ template <int KY, int KX, int NY, int NXP, int OFFXD>
 __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
 {
     constexpr int OUTS = 16 / KX;
-    constexpr int U = NY / cgcd(NY, KY);
+    constexpr int U = NY / cgcd(NY, KY);  // ring period (output rows)
     constexpr int D0 = floor4(OFFXD);
     constexpr int LAST = OFFXD + (OUTS - 1) * KX / 2 + NXP / 2;
     constexpr int NR = (LAST - D0 + 3) / 4;
@@ -274,26 +298,42 @@ __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
     const int BS = (rowDw + 2 * kPadW + 3) & ~3;
 
     for (int i = t; i < 2 * BS; i += static_cast<int>(blockDim.x)) {
-        int j = i % BS;
+        const int j = i < BS ? i : i - BS;
         if (j < kPadW || j >= kPadW + rowDw)
             lds[i] = 0;
     }
+    // border divisors, indexed per lane below: LDS keeps every read of them off the VMEM counter
+    int *btab = reinterpret_cast<int *>(lds + 2 * BS);
+    if (t < 64)
+        btab[t] = L.border[t];
 
     const int y0 = a.rowBegin + static_cast<int>(blockIdx.x) * a.rowsPerBand;
     const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
     if (y0 >= y1)
         return;
 
-    const uint8_t *srcF = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt + 16 * t;
-    uint8_t *dstF = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt + OUTS * t;
-    const int64_t srcSt = a.io.srcSt;
+    // Buffer descriptors over this frame's source window / destination band: row offsets are
+    // scalar (soffset), the lane offset is the only per-lane address term, and loads past the
+    // window return zero.
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, srcH = L.srcH;
+    const int voff = 16 * t;
 
+    // Branch-free row load: rows outside the image (r < 0 wraps to a huge unsigned soffset,
+    // r >= srcH lies past the range) are out of the descriptor's range and read as zero, which
+    // is exactly the masked border sum.  No branches keep the waitcnt counting exact, so the
+    // prefetch of the next rows stays in flight across the whole row.
+    (void)srcH;
+    const int dbg = a.dbg;
     auto load_row = [&](int r) -> uint4 {
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (active && r >= 0 && r < srcH)
-            v = load16_nt(srcF + static_cast<int64_t>(r - srcRow0) * srcSt);
-        return v;
+        u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, (dbg & 2) ? 0x7ff00000 : voff, (r - srcRow0) * srcSt,
+                                                        2 /* nt */);
+        return make_uint4(q.x, q.y, q.z, q.w);
     };
 
     uint32_t win[NY][8];
@@ -305,114 +345,120 @@ __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
     for (int j = 0; j < KY; ++j)
         pre[j] = load_row(KY * y0 + L.offY + NY - KY + j);
 
-    for (int yb = y0; yb < y1; yb += U) {
+    {
+        // Dropped store (out of range): makes the prologue end in the same VMEM pattern as the
+        // loop back-edge (loads, then one store), so the wait for `pre` is vmcnt(1) -- the
+        // previous row's store stays in flight -- instead of a conservative vmcnt(0).
+        u32x2 z = {0u, 0u};
+        __builtin_amdgcn_raw_buffer_store_b64(z, dstR, 0x7ff00000, 0, 0);
+    }
+    int phase = 0;  // position in the ring period: tap i of the current row lives in slot (phase*KY + i) % NY
+    for (int yy = y0; yy < y1; ++yy) {
+        uint32_t acc[8];
+        // ---- ring-dependent part, one static variant per phase (uniform branch)
         static_for<U>([&](auto uc) {
             constexpr int u = decltype(uc)::value;
-            const int yy = yb + u;
-            if (yy < y1) {
+            if (phase == u) {
 #pragma unroll
                 for (int j = 0; j < KY; ++j)
                     unpack16(pre[j], win[(u * KY + NY - KY + j) % NY]);
-                if (yy + 1 < y1) {
 #pragma unroll
-                    for (int j = 0; j < KY; ++j)
-                        pre[j] = load_row(KY * (yy + 1) + L.offY + NY - KY + j);
-                }
-                // ---- vertical taps (int16 wrap == low half of the packed u16 MAD)
-                uint32_t acc[8];
+                for (int j = 0; j < KY; ++j)  // (past the band end this reads unused rows)
+                    pre[j] = load_row(KY * (yy + 1) + L.offY + NY - KY + j);
+                // vertical taps: int16 wrap == low half of the packed u16 MAD.  Tap-outer /
+                // column-inner: gfx950 needs ~9 wait states between DEPENDENT v_pk_mad_u16, so
+                // the 8 independent column chains are interleaved to fill them.
 #pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    uint32_t s = pk_mul(win[(u * KY) % NY][c], L.cy[0]);
+                for (int c = 0; c < 8; ++c)
+                    acc[c] = pk_mul(win[(u * KY) % NY][c], L.cy[0]);
 #pragma unroll
-                    for (int i = 1; i < NY; ++i)
-                        s = pk_mad(win[(u * KY + i) % NY][c], L.cy[i], s);
-                    acc[c] = s;
-                }
-                uint32_t *row = lds + (yy & 1) * BS + kPadW;
-                if (active) {
-                    *reinterpret_cast<uint4 *>(row + 8 * t) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-                    *reinterpret_cast<uint4 *>(row + 8 * t + 4) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
-                    if (yy < L.mainBeginY || yy >= L.mainEndY) {
-                        // border row (uniform, rare): work = int16(int(nume) * 64 / deno), resizeYborder
-                        // :487-489.  Compact loop over this thread's own 16 LDS values.
-                        const int den = yy < L.mainBeginY ? L.border[yy] : L.border[16 + yy - L.mainEndY];
-                        uint32_t *w32 = row + 8 * t;
-#pragma unroll 1
-                        for (int c = 0; c < 8; ++c) {
-                            const uint32_t v = w32[c];
-                            const int lo = exact_div(static_cast<int>(static_cast<int16_t>(v & 0xffffu)) * 64, den);
-                            const int hi = exact_div(static_cast<int>(static_cast<int16_t>(v >> 16)) * 64, den);
-                            w32[c] = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
-                        }
-                    }
-                }
-                __syncthreads();
-                // ---- horizontal taps from LDS (int16 pairs . coefficient pairs -> int32)
-                uint32_t d[4 * NR];
-                const uint4 *b4 = reinterpret_cast<const uint4 *>(row + 8 * t + D0);
+                for (int i = 1; i < NY; ++i) {
 #pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    uint4 q = b4[r];
-                    d[4 * r + 0] = q.x;
-                    d[4 * r + 1] = q.y;
-                    d[4 * r + 2] = q.z;
-                    d[4 * r + 3] = q.w;
-                }
-                uint32_t ow[OUTS / 4];
-#pragma unroll
-                for (int k4 = 0; k4 < OUTS / 4; ++k4) {
-                    uint32_t word = 0;
-#pragma unroll
-                    for (int kk = 0; kk < 4; ++kk) {
-                        const int k = 4 * k4 + kk;
-                        int s = 1 << 19;
-#pragma unroll
-                        for (int p = 0; p < NXP / 2; ++p)
-                            s = sdot2(d[(KX * k) / 2 + OFFXD - D0 + p], L.cx[p], s);
-                        word |= opaque(static_cast<uint32_t>(clamp255(static_cast<int16_t>(s >> 20)))) << (8 * kk);
-                    }
-                    ow[k4] = word;
-                }
-                const int xbase = OUTS * t;
-                if (active && (xbase < L.mainBeginX || xbase + OUTS > L.mainEndX)) {
-                    // border columns (edge threads only): int16((nume + 2^19) / (deno * 64)),
-                    // resizeXborder :572 -- nume is the same dot product (invalid taps read the
-                    // zero pads), only the divisor differs.  Compact, not unrolled.
-                    auto w16 = [&](int c) {  // int16 work value at column c (c may be < 0: zero pad)
-                        const uint32_t v = row[c >> 1];
-                        return static_cast<int>(static_cast<int16_t>((c & 1) ? (v >> 16) : (v & 0xffffu)));
-                    };
-#pragma unroll 1
-                    for (int k = 0; k < OUTS; ++k) {
-                        const int x = xbase + k;
-                        if (x >= L.mainBeginX && x < L.mainEndX)
-                            continue;
-                        const int c0 = KX * x + L.offX;
-                        int s = 1 << 19;
-#pragma unroll 1
-                        for (int p = 0; p < NXP / 2; ++p) {
-                            const uint32_t cc = L.cx[p];
-                            s += w16(c0 + 2 * p) * static_cast<int16_t>(cc & 0xffffu) +
-                                 w16(c0 + 2 * p + 1) * static_cast<int16_t>(cc >> 16);
-                        }
-                        const int dv = x < L.mainBeginX ? L.border[32 + x] : L.border[48 + x - L.mainEndX];
-                        const uint32_t v = static_cast<uint32_t>(clamp255(static_cast<int16_t>(exact_div(s, dv))));
-                        const int sh = 8 * (k & 3);
-#pragma unroll
-                        for (int k4 = 0; k4 < OUTS / 4; ++k4)
-                            if ((k >> 2) == k4)
-                                ow[k4] = (ow[k4] & ~(0xffu << sh)) | (v << sh);
-                    }
-                }
-                if (active) {
-                    uint8_t *out = dstF + static_cast<int64_t>(yy - a.io.dstRow0) * a.io.dstSt;
-                    if constexpr (OUTS == 8)
-                        *reinterpret_cast<uint2 *>(out) = make_uint2(ow[0], ow[1]);
-                    else
-                        *reinterpret_cast<uint32_t *>(out) = ow[0];
+                    for (int c = 0; c < 8; ++c)
+                        acc[c] = pk_mad(win[(u * KY + i) % NY][c], L.cy[i], acc[c]);
                 }
             }
         });
+        phase = phase + 1 == U ? 0 : phase + 1;
+
+        uint32_t *row = lds + (yy & 1) * BS + kPadW;
+        if (active) {
+            *reinterpret_cast<uint4 *>(row + 8 * t) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+            *reinterpret_cast<uint4 *>(row + 8 * t + 4) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
+            if (yy < L.mainBeginY || yy >= L.mainEndY) {
+                // border row (uniform, rare): work = int16(int(nume) * 64 / deno)  (resizeYborder
+                // :487-489); invalid rows were loaded as zero, so nume is already the masked sum.
+                const int den = yy < L.mainBeginY ? btab[yy] : btab[16 + yy - L.mainEndY];
+                uint32_t *w32 = row + 8 * t;
+#pragma unroll 1
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t v = w32[c];
+                    const int lo = exact_div_fast(static_cast<int>(static_cast<int16_t>(v & 0xffffu)) * 64, den);
+                    const int hi = exact_div_fast(static_cast<int>(static_cast<int16_t>(v >> 16)) * 64, den);
+                    w32[c] = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
+                }
+            }
+        }
+        if (!(dbg & 4))
+            __syncthreads();
+        // ---- horizontal taps from LDS (int16 pairs . coefficient pairs -> int32)
+        uint32_t d[4 * NR];
+        const uint4 *b4 = reinterpret_cast<const uint4 *>(row + 8 * t + D0);
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            uint4 q = b4[r];
+            d[4 * r + 0] = q.x;
+            d[4 * r + 1] = q.y;
+            d[4 * r + 2] = q.z;
+            d[4 * r + 3] = q.w;
+        }
+        int sum[OUTS];
+#pragma unroll
+        for (int k = 0; k < OUTS; ++k) {
+            int s = 1 << 19;
+#pragma unroll
+            for (int p = 0; p < NXP / 2; ++p)
+                s = sdot2(d[(KX * k) / 2 + OFFXD - D0 + p], L.cx[p], s);
+            sum[k] = s;
+        }
+        int val[OUTS];
+#pragma unroll
+        for (int k = 0; k < OUTS; ++k)
+            val[k] = sum[k] >> 20;
+        const int xbase = OUTS * t;
+        if (active && (xbase < L.mainBeginX || xbase + OUTS > L.mainEndX)) {
+            // border columns (edge threads only): int16((nume + 2^19) / (deno * 64)),
+            // resizeXborder :572.  The dot product above already IS nume + 2^19 (invalid taps
+            // read the zero pads); only the divisor differs.
+#pragma unroll
+            for (int k = 0; k < OUTS; ++k) {
+                const int x = xbase + k;
+                if (x < L.mainBeginX)
+                    val[k] = exact_div_fast(sum[k], btab[32 + x]);
+                else if (x >= L.mainEndX)
+                    val[k] = exact_div_fast(sum[k], btab[48 + x - L.mainEndX]);
+            }
+        }
+        uint32_t ow[OUTS / 4];
+#pragma unroll
+        for (int k4 = 0; k4 < OUTS / 4; ++k4) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+                word |= opaque(static_cast<uint32_t>(clamp255(static_cast<int16_t>(val[4 * k4 + kk])))) << (8 * kk);
+            ow[k4] = word;
+        }
+        {
+            // unconditional store; inactive lanes aim past the range and are dropped
+            const int so = (yy - a.io.dstRow0) * dstSt;
+            const int vo = (active && !(dbg & 1)) ? OUTS * t : 0x7ff00000;
+            if constexpr (OUTS == 8) {
+                u32x2 o = {ow[0], ow[1]};
+                __builtin_amdgcn_raw_buffer_store_b64(o, dstR, vo, so, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b32(ow[0], dstR, vo, so, 0);
+            }
+        }
     }
 }
 
@@ -601,13 +647,22 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
         return hipSuccess;
     const int rows = rowEnd - rowBegin;
     bands = max(1, min(bands, rows));
-    LanczosArgs a{l, io, rowBegin, rowEnd, (rows + bands - 1) / bands};
+    LanczosArgs a{l, io, rowBegin, rowEnd, (rows + bands - 1) / bands, 0, 0, l.dbg};
+    // buffer ranges: the source window spans rows [srcRow0, srcH) of the frame, the destination
+    // band rows [rowBegin, rowEnd); both must be addressable with 32-bit offsets
+    const int64_t sb = static_cast<int64_t>(l.srcH - io.srcRow0 - 1) * io.srcSt + l.srcW;
+    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + l.dstW;
+    if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 31) ||
+        io.dstSt >= (int64_t(1) << 31))
+        return hipErrorInvalidValue;
+    a.srcBytes = static_cast<int>(sb);
+    a.dstBytes = static_cast<int>(db);
     bands = (rows + a.rowsPerBand - 1) / a.rowsPerBand;
     dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames));
     dim3 block(static_cast<unsigned>(lanczos_stream_block(l.srcW)));
     const int rowDw = l.srcW / 2;
     const int BS = (rowDw + 2 * kPadW + 3) & ~3;
-    size_t lds = static_cast<size_t>(2 * BS) * sizeof(uint32_t);
+    size_t lds = static_cast<size_t>(2 * BS + 64) * sizeof(uint32_t);
     if (l.NY == 10)
         hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3>), grid, block, lds, s, a);
     else

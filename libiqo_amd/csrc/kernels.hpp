@@ -39,6 +39,7 @@ struct LanczosDev {
     uint32_t cx[16];             // (c_2p, c_2p+1) int16 pairs
     int mainBeginY, mainEndY, mainBeginX, mainEndX;
     const int *border;           // device: [0,16) denoYTop, [16,32) denoYBot, [32,48) dXLeft, [48,64) dXRight
+    int dbg;                     // timing experiments only (see kernels.hip)
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
