@@ -106,6 +106,10 @@ def cpu_baseline(cfg, frame_np, seconds, threads):
             "seconds": round(t1 + tn, 2)}
 
 
+def kernel_is_lanczos(method, r):
+    return method == "lanczos" and r.describe()["kernel"] == "lanczos_stream"
+
+
 def read_pmc(config):
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % config)
     try:
@@ -128,6 +132,7 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--force-general", action="store_true")
     ap.add_argument("--debug-flags", type=int, default=0, help="timing experiments (wrong output)")
+    ap.add_argument("--prefetch", type=int, default=0, help="Lanczos streamer prefetch depth (0 = default)")
     args = ap.parse_args()
 
     import torch
@@ -157,6 +162,8 @@ def main():
         r.set_option("force_general", 1)
     if args.debug_flags:
         r.set_option("debug_flags", args.debug_flags)
+    if args.prefetch and kernel_is_lanczos(m, r):
+        r.set_option("prefetch", args.prefetch)
     kernel = r.describe()["kernel"]
 
     gen = torch.Generator(device=dev)
@@ -214,7 +221,7 @@ def main():
         cpu = cpu_baseline(cfg, src[0].cpu().numpy(), args.cpu_seconds, threads)
 
     if rank == 0:
-        out_px = float(frames) * dw * dh * world
+        out_px = float(frames) * dw * dh * world * args.steps
         value = out_px / wall_max / 1e6
         bytes_launch = float(frames) * (sw * sh + dw * dh)
         achieved = bytes_launch / (kern_ms / 1e3) / 1e9

@@ -16,7 +16,8 @@ __all__ = ["IqoError", "LanczosResizer", "AreaResizer", "LinearResizer", "availa
            "host_tables", "host_kernel_for", "KERNELS", "LIB_PATH"]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libiqo_hip.so")
+# LIBIQO_AMD_LIB selects an alternative build of the same library (A/B experiments only)
+LIB_PATH = os.environ.get("LIBIQO_AMD_LIB") or os.path.join(PKG_DIR, "libiqo_hip.so")
 
 KERNELS = {0: "general", 1: "lanczos_stream", 2: "area_int", 3: "linear_up2"}
 _METHODS = {"lanczos": 0, "area": 1, "linear": 2}

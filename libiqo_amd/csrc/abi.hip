@@ -32,6 +32,7 @@ struct iqo_hip_plan {
     bool forceGeneral = false;
     int bands = 0;
     int debugFlags = 0;
+    int prefetch = 2;
     hipStream_t stream = nullptr;
     uint8_t *stageSrc = nullptr, *stageDst = nullptr;
     size_t stageSrcCap = 0, stageDstCap = 0;
@@ -280,6 +281,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             l.mainEndX = f.mainEndX;
             l.border = h->dBorder;
             l.dbg = h->debugFlags;
+            l.prefetch = h->prefetch;
             int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
             e = iqo_amd::launch_lanczos_stream(l, io, rb, re, bands, s);
         } else if (kernel == IQO_KERNEL_AREA_INT) {
@@ -395,6 +397,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "debug_flags")) {  // timing experiments only: results are wrong
         h->debugFlags = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "prefetch")) {  // Lanczos streamer prefetch depth (rows)
+        if (value < 1 || value > 3)
+            return IQO_HIP_EINVAL;
+        h->prefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "bands")) {

@@ -270,147 +270,163 @@ struct LanczosArgs {
     Io io;
     int rowBegin, rowEnd, rowsPerBand;
     int srcBytes, dstBytes;  // extent of one frame's source window / destination band (buffer range)
+    int bands, wavesPerRow;  // wave grid per frame: band-major, column-minor
     int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
                              // 2 = no prefetch loads, 4 = no barrier.  0 in production.
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
-constexpr int floor4(int v) { return v >= 0 ? (v / 4) * 4 : -(((-v) + 3) / 4) * 4; }
-constexpr int kPadW = 8;  // zero dwords left and right of each LDS work row
 
-template <int KY, int KX, int NY, int NXP, int OFFXD>
-__global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
+template <int KY, int KX, int NY, int NXP, int OFFXD, int PD>
+__global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 {
-    constexpr int OUTS = 16 / KX;
-    constexpr int U = NY / cgcd(NY, KY);  // ring period (output rows)
-    constexpr int D0 = floor4(OFFXD);
-    constexpr int LAST = OFFXD + (OUTS - 1) * KX / 2 + NXP / 2;
-    constexpr int NR = (LAST - D0 + 3) / 4;
-    static_assert(D0 >= -kPadW && D0 + 4 * NR - 8 <= kPadW, "LDS pad too small");
+    constexpr int OUTS = 16 / KX;            // outputs per producing lane
+    constexpr int OPW = 62 * OUTS;           // outputs per wave (lanes 1..62)
+    constexpr int P = NY / KY;               // output rows pending at once (accumulator ring)
+    static_assert(NY % KY == 0, "NY must be a multiple of KY");
+    constexpr int LV = P * PD / cgcd(P, PD);  // static variants: accumulator slot x prefetch slot
+    constexpr int DLO = OFFXD;               // first work dword a lane reads, relative to its own
+    constexpr int DHI = (OUTS - 1) * KX / 2 + OFFXD + NXP / 2;  // one past the last
+    static_assert(DLO >= -8 && DHI <= 16, "horizontal taps must stay within the neighbouring lanes");
     static_assert(OUTS == 8 || OUTS == 4, "");
 
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const LanczosDev &L = a.l;
-    const int t = static_cast<int>(threadIdx.x);
-    const int nthr = L.srcW >> 4;
-    const bool active = t < nthr;
-    const int rowDw = L.srcW >> 1;
-    const int BS = (rowDw + 2 * kPadW + 3) & ~3;
-
-    for (int i = t; i < 2 * BS; i += static_cast<int>(blockDim.x)) {
-        const int j = i < BS ? i : i - BS;
-        if (j < kPadW || j >= kPadW + rowDw)
-            lds[i] = 0;
-    }
-    // border divisors, indexed per lane below: LDS keeps every read of them off the VMEM counter
-    int *btab = reinterpret_cast<int *>(lds + 2 * BS);
-    if (t < 64)
-        btab[t] = L.border[t];
-
-    const int y0 = a.rowBegin + static_cast<int>(blockIdx.x) * a.rowsPerBand;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = static_cast<int>(threadIdx.x) >> 6;  // wave in block
+    const int g = static_cast<int>(blockIdx.x) * 4 + wib;  // wave index in the (band, column) grid
+    if (g >= a.bands * a.wavesPerRow)
+        return;  // whole wave: nothing below synchronises across waves
+    const int band = g / a.wavesPerRow, wcol = g - band * a.wavesPerRow;
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
     const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
     if (y0 >= y1)
         return;
 
-    // Buffer descriptors over this frame's source window / destination band: row offsets are
-    // scalar (soffset), the lane offset is the only per-lane address term, and loads past the
-    // window return zero.
+    // per-wave copy of the border divisors (read with per-lane indices; LDS keeps them off the
+    // VMEM counter); only this wave touches its copy, so no barrier is needed
+    __shared__ int btabs[4][64];
+    int *btab = btabs[wib];
+    btab[lane] = L.border[lane];
+
+    const int x0 = wcol * OPW;                    // first output column of lane 1
+    const int cb = KX * x0 - 16 + 16 * lane;      // first source column of this lane's block
+    const int outX = x0 + (lane - 1) * OUTS;      // first output column of this lane
+    const bool produce = lane >= 1 && lane <= 62 && outX < L.dstW;
+    const int voff = (cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;  // off-image blocks read zero
+    (void)outX;
+
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
     const __amdgpu_buffer_rsrc_t srcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
-    const int srcRow0 = a.io.srcRow0, srcH = L.srcH;
-    const int voff = 16 * t;
+    const int srcRow0 = a.io.srcRow0;
+    const int dbg = a.dbg;
 
     // Branch-free row load: rows outside the image (r < 0 wraps to a huge unsigned soffset,
-    // r >= srcH lies past the range) are out of the descriptor's range and read as zero, which
-    // is exactly the masked border sum.  No branches keep the waitcnt counting exact, so the
-    // prefetch of the next rows stays in flight across the whole row.
-    (void)srcH;
-    const int dbg = a.dbg;
+    // r >= srcH lies past the range) and off-image column blocks are outside the descriptor's
+    // range and read as zero -- exactly the masked border sums.  No branches keep the waitcnt
+    // counting exact, so the next rows' prefetch stays in flight across the whole row.
     auto load_row = [&](int r) -> uint4 {
         u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, (dbg & 2) ? 0x7ff00000 : voff, (r - srcRow0) * srcSt,
                                                         2 /* nt */);
         return make_uint4(q.x, q.y, q.z, q.w);
     };
 
-    uint32_t win[NY][8];
+    // Accumulator ring: each source row, as it arrives, is multiplied into the partial sums of
+    // the P output rows that still need it (tap NY-KY*(q+1)+j for the q-th pending row).  Row
+    // yy completes in slot yy mod P.  Iterations start P-1 rows early to prime the ring.
+    uint32_t accR[P][8];
 #pragma unroll
-    for (int i = 0; i < NY - KY; ++i)
-        unpack16(load_row(KY * y0 + L.offY + i), win[i]);
-    uint4 pre[KY];
+    for (int q = 0; q < P; ++q)
 #pragma unroll
-    for (int j = 0; j < KY; ++j)
-        pre[j] = load_row(KY * y0 + L.offY + NY - KY + j);
-
+        for (int c = 0; c < 8; ++c)
+            accR[q][c] = 0;
+    const int yStart = y0 - (P - 1);
+    // prefetch ring: the source rows of iteration `it` live in slot it % PD; they are issued PD
+    // iterations ahead (static slots: moving a register with a load in flight would force a wait)
+    uint4 pre[PD][KY];
+#pragma unroll
+    for (int i = 0; i < PD; ++i)
+#pragma unroll
+        for (int j = 0; j < KY; ++j)
+            pre[i][j] = load_row(KY * (yStart + i) + L.offY + NY - KY + j);
     {
         // Dropped store (out of range): makes the prologue end in the same VMEM pattern as the
-        // loop back-edge (loads, then one store), so the wait for `pre` is vmcnt(1) -- the
-        // previous row's store stays in flight -- instead of a conservative vmcnt(0).
+        // loop back-edge (loads, then one store) so waits for `pre` stay counted, not vmcnt(0).
         u32x2 z = {0u, 0u};
         __builtin_amdgcn_raw_buffer_store_b64(z, dstR, 0x7ff00000, 0, 0);
     }
-    int phase = 0;  // position in the ring period: tap i of the current row lives in slot (phase*KY + i) % NY
-    for (int yy = y0; yy < y1; ++yy) {
+
+    int phase = 0;  // == (yy - yStart) mod LV; row yy completes in accumulator slot phase % P
+    for (int yy = yStart; yy < y1; ++yy) {
         uint32_t acc[8];
         // ---- ring-dependent part, one static variant per phase (uniform branch)
-        static_for<U>([&](auto uc) {
-            constexpr int u = decltype(uc)::value;
-            if (phase == u) {
+        static_for<LV>([&](auto uc) {
+            constexpr int v = decltype(uc)::value;
+            constexpr int u = v % P;   // accumulator slot of row yy
+            constexpr int ps = v % PD; // prefetch slot holding row yy's new source rows
+            if (phase == v) {
+                uint32_t nw[KY][8];
 #pragma unroll
                 for (int j = 0; j < KY; ++j)
-                    unpack16(pre[j], win[(u * KY + NY - KY + j) % NY]);
+                    unpack16(pre[ps][j], nw[j]);
 #pragma unroll
                 for (int j = 0; j < KY; ++j)  // (past the band end this reads unused rows)
-                    pre[j] = load_row(KY * (yy + 1) + L.offY + NY - KY + j);
-                // vertical taps: int16 wrap == low half of the packed u16 MAD.  Tap-outer /
-                // column-inner: gfx950 needs ~9 wait states between DEPENDENT v_pk_mad_u16, so
-                // the 8 independent column chains are interleaved to fill them.
+                    pre[ps][j] = load_row(KY * (yy + PD) + L.offY + NY - KY + j);
+                // vertical taps: int16 wrap == low half of the packed u16 MAD.  The q loop is
+                // inside the column loop's outer level so the 8 independent column chains stay
+                // interleaved (gfx950 wants ~9 wait states between DEPENDENT v_pk_mad_u16).
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    constexpr int dummy = 0;
+                    (void)dummy;
+#pragma unroll
+                    for (int j = 0; j < KY; ++j) {
+                        const uint32_t cq = L.cy[NY - KY * (q + 1) + j];
+                        uint32_t *ar = accR[(u + q) % P];
+#pragma unroll
+                        for (int c = 0; c < 8; ++c)
+                            ar[c] = (q == P - 1 && j == 0) ? pk_mul(nw[j][c], cq) : pk_mad(nw[j][c], cq, ar[c]);
+                    }
+                }
 #pragma unroll
                 for (int c = 0; c < 8; ++c)
-                    acc[c] = pk_mul(win[(u * KY) % NY][c], L.cy[0]);
-#pragma unroll
-                for (int i = 1; i < NY; ++i) {
-#pragma unroll
-                    for (int c = 0; c < 8; ++c)
-                        acc[c] = pk_mad(win[(u * KY + i) % NY][c], L.cy[i], acc[c]);
-                }
+                    acc[c] = accR[u][c];
+                // distinct per phase: stops the compiler from tail-merging the P structurally
+                // identical variants into one block fed by register shuffles (seen: scratch spills)
+                asm volatile("; ring phase %0" ::"n"(v));
             }
         });
-        phase = phase + 1 == U ? 0 : phase + 1;
+        phase = phase + 1 == LV ? 0 : phase + 1;
+        if (yy < y0)
+            continue;  // priming iterations (uniform)
 
-        uint32_t *row = lds + (yy & 1) * BS + kPadW;
-        if (active) {
-            *reinterpret_cast<uint4 *>(row + 8 * t) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
-            *reinterpret_cast<uint4 *>(row + 8 * t + 4) = make_uint4(acc[4], acc[5], acc[6], acc[7]);
-            if (yy < L.mainBeginY || yy >= L.mainEndY) {
-                // border row (uniform, rare): work = int16(int(nume) * 64 / deno)  (resizeYborder
-                // :487-489); invalid rows were loaded as zero, so nume is already the masked sum.
-                const int den = yy < L.mainBeginY ? btab[yy] : btab[16 + yy - L.mainEndY];
-                uint32_t *w32 = row + 8 * t;
-#pragma unroll 1
-                for (int c = 0; c < 8; ++c) {
-                    const uint32_t v = w32[c];
-                    const int lo = exact_div_fast(static_cast<int>(static_cast<int16_t>(v & 0xffffu)) * 64, den);
-                    const int hi = exact_div_fast(static_cast<int>(static_cast<int16_t>(v >> 16)) * 64, den);
-                    w32[c] = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
-                }
+        if (yy < L.mainBeginY || yy >= L.mainEndY) {
+            // border row (uniform, rare): work = int16(int(nume) * 64 / deno) (resizeYborder
+            // :487-489); invalid rows were read as zero, so nume is already the masked sum.
+            const int den = yy < L.mainBeginY ? btab[yy] : btab[16 + yy - L.mainEndY];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int lo = exact_div_fast(static_cast<int>(static_cast<int16_t>(acc[c] & 0xffffu)) * 64, den);
+                const int hi = exact_div_fast(static_cast<int>(static_cast<int16_t>(acc[c] >> 16)) * 64, den);
+                acc[c] = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
             }
         }
-        if (!(dbg & 4))
-            __syncthreads();
-        // ---- horizontal taps from LDS (int16 pairs . coefficient pairs -> int32)
-        uint32_t d[4 * NR];
-        const uint4 *b4 = reinterpret_cast<const uint4 *>(row + 8 * t + D0);
+
+        // ---- neighbour work columns by DPP (lane l-1 / l+1), then horizontal taps
+        uint32_t d[DHI - DLO];
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            uint4 q = b4[r];
-            d[4 * r + 0] = q.x;
-            d[4 * r + 1] = q.y;
-            d[4 * r + 2] = q.z;
-            d[4 * r + 3] = q.w;
+        for (int j = DLO; j < DHI; ++j) {
+            if (j < 0)
+                d[j - DLO] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc[8 + j]),
+                                                                               0x138 /* wave_shr:1 */, 0xf, 0xf, false));
+            else if (j >= 8)
+                d[j - DLO] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc[j - 8]),
+                                                                               0x130 /* wave_shl:1 */, 0xf, 0xf, false));
+            else
+                d[j - DLO] = acc[j];
         }
         int sum[OUTS];
 #pragma unroll
@@ -418,21 +434,20 @@ __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
             int s = 1 << 19;
 #pragma unroll
             for (int p = 0; p < NXP / 2; ++p)
-                s = sdot2(d[(KX * k) / 2 + OFFXD - D0 + p], L.cx[p], s);
+                s = sdot2(d[(KX * k) / 2 + OFFXD - DLO + p], L.cx[p], s);
             sum[k] = s;
         }
         int val[OUTS];
 #pragma unroll
         for (int k = 0; k < OUTS; ++k)
             val[k] = sum[k] >> 20;
-        const int xbase = OUTS * t;
-        if (active && (xbase < L.mainBeginX || xbase + OUTS > L.mainEndX)) {
-            // border columns (edge threads only): int16((nume + 2^19) / (deno * 64)),
-            // resizeXborder :572.  The dot product above already IS nume + 2^19 (invalid taps
-            // read the zero pads); only the divisor differs.
+        if (produce && (outX < L.mainBeginX || outX + OUTS > L.mainEndX)) {
+            // border columns (edge lanes only): int16((nume + 2^19) / (deno * 64)),
+            // resizeXborder :572.  The dot product above already IS nume + 2^19 (off-image
+            // taps read zero); only the divisor differs.
 #pragma unroll
             for (int k = 0; k < OUTS; ++k) {
-                const int x = xbase + k;
+                const int x = outX + k;
                 if (x < L.mainBeginX)
                     val[k] = exact_div_fast(sum[k], btab[32 + x]);
                 else if (x >= L.mainEndX)
@@ -449,9 +464,9 @@ __global__ __launch_bounds__(512) void lanczos_stream_kernel(LanczosArgs a)
             ow[k4] = word;
         }
         {
-            // unconditional store; inactive lanes aim past the range and are dropped
+            // unconditional store; non-producing lanes aim past the range and are dropped
             const int so = (yy - a.io.dstRow0) * dstSt;
-            const int vo = (active && !(dbg & 1)) ? OUTS * t : 0x7ff00000;
+            const int vo = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
             if constexpr (OUTS == 8) {
                 u32x2 o = {ow[0], ow[1]};
                 __builtin_amdgcn_raw_buffer_store_b64(o, dstR, vo, so, 0);
@@ -638,7 +653,7 @@ bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)
     return KY == 2 && KX == 2 && ((NY == 10 && NXP == 14 && offX == -6) || (NY == 8 && NXP == 10 && offX == -4));
 }
 
-int lanczos_stream_block(int srcW) { return ((srcW / 16 + 63) / 64) * 64; }
+int lanczos_stream_block(int) { return 256; }
 
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
                                  hipStream_t s)
@@ -647,9 +662,13 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
         return hipSuccess;
     const int rows = rowEnd - rowBegin;
     bands = max(1, min(bands, rows));
-    LanczosArgs a{l, io, rowBegin, rowEnd, (rows + bands - 1) / bands, 0, 0, l.dbg};
+    const int rpb = (rows + bands - 1) / bands;
+    bands = (rows + rpb - 1) / rpb;
+    const int opw = 62 * (16 / l.KX);
+    const int wpr = (l.dstW + opw - 1) / opw;
+    LanczosArgs a{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg};
     // buffer ranges: the source window spans rows [srcRow0, srcH) of the frame, the destination
-    // band rows [rowBegin, rowEnd); both must be addressable with 32-bit offsets
+    // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(l.srcH - io.srcRow0 - 1) * io.srcSt + l.srcW;
     const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + l.dstW;
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 31) ||
@@ -657,16 +676,24 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
         return hipErrorInvalidValue;
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
-    bands = (rows + a.rowsPerBand - 1) / a.rowsPerBand;
-    dim3 grid(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames));
-    dim3 block(static_cast<unsigned>(lanczos_stream_block(l.srcW)));
-    const int rowDw = l.srcW / 2;
-    const int BS = (rowDw + 2 * kPadW + 3) & ~3;
-    size_t lds = static_cast<size_t>(2 * BS + 64) * sizeof(uint32_t);
-    if (l.NY == 10)
-        hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3>), grid, block, lds, s, a);
-    else
-        hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2>), grid, block, lds, s, a);
+    const int waves = bands * wpr;
+    dim3 grid(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    const int pd = l.prefetch;
+    if (l.NY == 10) {
+        if (pd <= 1)
+            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 1>), grid, dim3(256), 0, s, a);
+        else if (pd == 2)
+            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 2>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 3>), grid, dim3(256), 0, s, a);
+    } else {
+        if (pd <= 1)
+            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2, 1>), grid, dim3(256), 0, s, a);
+        else if (pd == 2)
+            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2, 2>), grid, dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2, 3>), grid, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -40,6 +40,7 @@ struct LanczosDev {
     int mainBeginY, mainEndY, mainBeginX, mainEndX;
     const int *border;           // device: [0,16) denoYTop, [16,32) denoYBot, [32,48) dXLeft, [48,64) dXRight
     int dbg;                     // timing experiments only (see kernels.hip)
+    int prefetch;                // prefetch depth in output rows (1..3)
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
