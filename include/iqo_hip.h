@@ -114,6 +114,11 @@ const char *iqo_hip_version(void);
 int iqo_host_tables(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                     size_t pxScale, int axis, int *nTaps, int *nPhases, int32_t *buf, size_t cap);
 
+/* Host-only twin of iqo_hip_band_src_rows (no device needed): the source-row halo of output rows
+ * [dstRow0, dstRow0 + dstRows) for the given resizer shape. */
+int iqo_host_band_src_rows(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                           size_t pxScale, size_t dstRow0, size_t dstRows, size_t *srcRow0, size_t *srcRows);
+
 /* Host-only: which kernel family a full-frame, 16-byte-aligned device call would use. */
 int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                         size_t pxScale);

@@ -13,7 +13,7 @@ import ctypes
 import os
 
 __all__ = ["IqoError", "LanczosResizer", "AreaResizer", "LinearResizer", "available", "lib",
-           "host_tables", "host_kernel_for", "KERNELS", "LIB_PATH"]
+           "host_tables", "host_kernel_for", "host_band_src_rows", "KERNELS", "LIB_PATH"]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # LIBIQO_AMD_LIB selects an alternative build of the same library (A/B experiments only)
@@ -68,6 +68,8 @@ def lib():
                                   ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                   ctypes.POINTER(ctypes.c_int32), _c_sz]
     L.iqo_host_kernel_for.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz]
+    L.iqo_host_band_src_rows.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz,
+                                         ctypes.POINTER(_c_sz), ctypes.POINTER(_c_sz)]
     _lib = L
     return L
 
@@ -95,6 +97,14 @@ def host_tables(method, degree, srcW, srcH, dstW, dstH, pxScale, axis):
                       ctypes.byref(nt), ctypes.byref(npz), buf, total)
     rows = [list(buf[q * nt.value:(q + 1) * nt.value]) for q in range(npz.value)]
     return rows
+
+
+def host_band_src_rows(method, degree, srcW, srcH, dstW, dstH, pxScale, dstRow0, dstRows):
+    """Source-row window (srcRow0, srcRows) read by output rows [dstRow0, dstRow0+dstRows) -- host only."""
+    a, b = _c_sz(), _c_sz()
+    _check(lib().iqo_host_band_src_rows(_METHODS[method], degree, srcW, srcH, dstW, dstH, pxScale, dstRow0, dstRows,
+                                        ctypes.byref(a), ctypes.byref(b)), "host_band_src_rows")
+    return a.value, b.value
 
 
 def host_kernel_for(method, degree, srcW, srcH, dstW, dstH, pxScale=1):

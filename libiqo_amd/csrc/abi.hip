@@ -529,6 +529,24 @@ int iqo_host_tables(int method, unsigned degree, size_t srcW, size_t srcH, size_
     return static_cast<int>(a.table.size());
 }
 
+int iqo_host_band_src_rows(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                           size_t pxScale, size_t dstRow0, size_t dstRows, size_t *srcRow0, size_t *srcRows)
+{
+    if (method < 0 || method > 2 || !srcRow0 || !srcRows)
+        return IQO_HIP_EINVAL;
+    Plan p;
+    std::string err;
+    if (!iqo_amd::build_plan(static_cast<iqo_amd::Method>(method), degree, srcW, srcH, dstW, dstH, pxScale, &p, &err))
+        return IQO_HIP_EINVAL;
+    if (dstRow0 + dstRows > dstH)
+        return IQO_HIP_EINVAL;
+    int s0, s1;
+    iqo_amd::band_src_rows(p, static_cast<int>(dstRow0), static_cast<int>(dstRow0 + dstRows), &s0, &s1);
+    *srcRow0 = static_cast<size_t>(s0);
+    *srcRows = static_cast<size_t>(s1 - s0);
+    return IQO_HIP_OK;
+}
+
 int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH, size_t pxScale)
 {
     if (method < 0 || method > 2)
