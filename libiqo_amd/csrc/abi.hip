@@ -32,7 +32,7 @@ struct iqo_hip_plan {
     bool forceGeneral = false;
     int bands = 0;
     int debugFlags = 0;
-    int prefetch = 2;
+    int prefetch = 1;  // best of the 1/2/3 sweep on C2 (profiles/r01)
     hipStream_t stream = nullptr;
     uint8_t *stageSrc = nullptr, *stageDst = nullptr;
     size_t stageSrcCap = 0, stageDstCap = 0;

@@ -871,9 +871,12 @@ void iqo_gen_g1(uint8_t *p, size_t w, size_t h, size_t st)
             p[y * st + x] = (uint8_t)(((uint32_t)(y * w + x) * 2654435761u) >> 24);
 }
 
-/* std::mt19937(seed) + std::uniform_int_distribution<int>(0,255) as in libstdc++
- * (benchmark/benchmark.cpp:51-59): MT19937 then the "downscaling" rejection
- * (scaling = 0xffffffff / 256, reject >= 256*scaling). */
+/* std::mt19937(seed) + std::uniform_int_distribution<int>(0,255) as the benchmark draws its planes
+ * (benchmark/benchmark.cpp:51-59), with the mapping of this image's libstdc++ (GCC >= 11): for a
+ * full-range 32-bit engine, uniform_int_distribution uses Lemire's nearly-divisionless method,
+ * product = r * 256 (64-bit), reject while low32(product) < (2^32 - 256) % 256 (= 0: never),
+ * result = product >> 32 = r >> 24.  (The older divide-and-reject mapping, r / (0xffffffff/256),
+ * differs from the 75489th draw on.) */
 void iqo_gen_mt19937(uint8_t *p, size_t n, uint32_t seed)
 {
     uint32_t mt[624];
@@ -881,10 +884,10 @@ void iqo_gen_mt19937(uint8_t *p, size_t n, uint32_t seed)
     mt[0] = seed;
     for (int i = 1; i < 624; ++i)
         mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
-    const uint32_t scaling = 0xffffffffu / 256u;
-    const uint32_t past = 256u * scaling;
+    const uint64_t range = 256u;
+    const uint32_t threshold = (uint32_t)(0u - (uint32_t)range) % (uint32_t)range;
     for (size_t k = 0; k < n; ++k) {
-        uint32_t r;
+        uint64_t prod;
         do {
             if (idx >= 624) {
                 for (int i = 0; i < 624; ++i) {
@@ -898,9 +901,9 @@ void iqo_gen_mt19937(uint8_t *p, size_t n, uint32_t seed)
             y ^= (y << 7) & 0x9d2c5680u;
             y ^= (y << 15) & 0xefc60000u;
             y ^= y >> 18;
-            r = y;
-        } while (r >= past);
-        p[k] = (uint8_t)(r / scaling);
+            prod = (uint64_t)y * range;
+        } while ((uint32_t)prod < threshold);
+        p[k] = (uint8_t)(prod >> 32);
     }
 }
 

@@ -185,3 +185,24 @@ def test_many_frames_grid_chunking():
     for f in (0, 65534, 65535, 69999):
         exp = ol.run_oracle(m, d, sw, sh, dw, dh, px, src[f].cpu().numpy())
         assert (out[f].cpu().numpy() == exp).all(), f
+
+
+@pytest.mark.parametrize("m,iw,ih,ow,oh", [("lanczos2", 640, 480, 320, 240), ("lanczos3", 3840, 2160, 1920, 1080),
+                                           ("area", 7680, 4320, 1920, 1080), ("linear", 1920, 1080, 3840, 2160)])
+def test_cpp_dropin_benchmark_cli(tmp_path, m, iw, ih, ow, oh):
+    """The reference-compatible benchmark CLI (benchmark/iqo_benchmark.cpp), built against the
+    drop-in iqo::*Resizer classes, produces the Generic output on the benchmark's own input
+    (std::mt19937(0) Y plane, benchmark.cpp:51-59)."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(libiqo_amd.LIB_PATH), "build", "iqo_benchmark")
+    out = tmp_path / "y.raw"
+    r = subprocess.run([exe, "-m", m, "-iw", str(iw), "-ih", str(ih), "-ow", str(ow), "-oh", str(oh),
+                        "-cycles", "2", "-check", str(out)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ms/cycle" in r.stdout
+    got = np.fromfile(str(out), dtype=np.uint8).reshape(oh, ow)
+    method = "lanczos" if m.startswith("lanczos") else m
+    degree = int(m[7]) if method == "lanczos" else 0
+    exp = ol.run_oracle(method, degree, iw, ih, ow, oh, 1, ol.gen("mt19937", iw, ih))
+    assert (got == exp).all()
