@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Turn the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_ci.sh (pmc) into
+profiles/pmc_<cfg>.json, which bench.py reads for roofline.traffic.
+
+HBM bytes per launch follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are in
+KiB; on gfx950 FETCH_SIZE counts exactly 1/2 of the bytes of a wide coalesced streaming read, so
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+The two counters come from separate passes (they do not fit one TCC pass); each is the median
+over the profiled dispatches of the hot kernel.
+
+  python scripts/pmc_to_json.py gpurun_out c2 c3 c4 [--round r01]
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+KERNELS = {"lanczos_stream": "lanczos_stream_kernel", "area_int": "area_int_kernel",
+           "linear_up2": "linear_up2_kernel", "general": "general_kernel"}
+BENCH = {"c2": ("lanczos_stream", 128), "c3": ("area_int", 48), "c4": ("linear_up2", 128), "c1": ("lanczos_stream", 4096)}
+
+
+def per_dispatch(dirname, counter, kname):
+    files = glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True)
+    vals = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter or kname not in row.get("Kernel_Name", ""):
+                    continue
+                d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rnd = "r01"
+    if "--round" in sys.argv:
+        rnd = sys.argv[sys.argv.index("--round") + 1]
+        args.remove(rnd)
+    out_dir, cfgs = args[0], args[1:]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for c in cfgs:
+        kernel, frames = BENCH[c]
+        kname = KERNELS[kernel]
+        fetch = per_dispatch(os.path.join(out_dir, "pmc_fetch_" + c), "FETCH_SIZE", kname)
+        write = per_dispatch(os.path.join(out_dir, "pmc_write_" + c), "WRITE_SIZE", kname)
+        if not fetch or not write:
+            print("%s: no counter rows for %s" % (c, kname))
+            continue
+        f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+        res = {"config": c, "kernel": kernel, "frames": frames, "round": rnd,
+               "fetch_size_kib": f_kib, "write_size_kib": w_kib, "dispatches": [len(fetch), len(write)],
+               "hbm_read_bytes_per_launch": int(2 * f_kib * 1024), "hbm_write_bytes_per_launch": int(w_kib * 1024),
+               "hbm_bytes_per_launch": int((2 * f_kib + w_kib) * 1024),
+               "correction": "read = 2 x FETCH_SIZE (gfx950 half-count), KiB -> bytes x1024"}
+        with open(os.path.join(root, "profiles", "pmc_%s.json" % c), "w") as f:
+            json.dump(res, f, indent=1)
+        print(c, json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
