@@ -1,7 +1,7 @@
 // abi.hip -- implementation of include/iqo_hip.h (the extern "C" boundary).
 //
 // A plan owns: the host Plan (tables + index maps, plan.cpp), their device copies, the chunk
-// table of the general kernel, the border tables of the Lanczos streamer, and (lazily) a stream
+// table of the general kernel, and (lazily) a stream
 // plus device staging buffers for the host-pointer entry point.  There is no CPU fallback:
 // any HIP failure is returned as a negative status.
 #include "iqo_hip.h"
@@ -27,12 +27,12 @@ struct iqo_hip_plan {
     Plan p;
     int device = 0;
     int4 *dX = nullptr, *dY = nullptr, *dChunks = nullptr;
-    int *dTabX = nullptr, *dTabY = nullptr, *dBorder = nullptr;
+    int *dTabX = nullptr, *dTabY = nullptr;
     int nChunks = 0, ldsInts = 0;
     bool forceGeneral = false;
     int bands = 0;
     int debugFlags = 0;
-    int prefetch = 1;  // best of the 1/2/3 sweep on C2 (profiles/r01)
+    int prefetch = 3;  // best of the 1/2/3 sweep on C2 (straight-line streamer)
     hipStream_t stream = nullptr;
     uint8_t *stageSrc = nullptr, *stageDst = nullptr;
     size_t stageSrcCap = 0, stageDstCap = 0;
@@ -136,7 +136,6 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dChunks);
     (void)hipFree(h->dTabX);
     (void)hipFree(h->dTabY);
-    (void)hipFree(h->dBorder);
     (void)hipFree(h->stageSrc);
     (void)hipFree(h->stageDst);
     if (h->stream)
@@ -185,21 +184,10 @@ int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t d
     }
     h->nChunks = static_cast<int>(chunks.size());
     std::vector<int4> xr = coord_records(h->p.x), yr = coord_records(h->p.y);
-    std::vector<int> border(64, 0);
-    const iqo_amd::FastLanczos &f = h->p.flz;
-    for (size_t i = 0; i < f.denoYTop.size() && i < 16; ++i)
-        border[i] = f.denoYTop[i];
-    for (size_t i = 0; i < f.denoYBot.size() && i < 16; ++i)
-        border[16 + i] = f.denoYBot[i];
-    for (size_t i = 0; i < f.dXLeft.size() && i < 16; ++i)
-        border[32 + i] = f.dXLeft[i];
-    for (size_t i = 0; i < f.dXRight.size() && i < 16; ++i)
-        border[48 + i] = f.dXRight[i];
     if ((rc = upload(&h->dX, xr.data(), xr.size())) || (rc = upload(&h->dY, yr.data(), yr.size())) ||
         (rc = upload(&h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
         (rc = upload(&h->dTabY, h->p.y.table.data(), h->p.y.table.size())) ||
-        (rc = upload(&h->dChunks, chunks.data(), chunks.size())) ||
-        (rc = upload(&h->dBorder, border.data(), border.size()))) {
+        (rc = upload(&h->dChunks, chunks.data(), chunks.size()))) {
         free_plan(h);
         return rc;
     }
@@ -279,7 +267,16 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             l.mainEndY = f.mainEndY;
             l.mainBeginX = f.mainBeginX;
             l.mainEndX = f.mainEndX;
-            l.border = h->dBorder;
+            for (int i = 0; i < 16; ++i) {
+                l.yTopM[i] = f.yTopM[i];
+                l.yTopS[i] = f.yTopS[i];
+                l.yBotM[i] = f.yBotM[i];
+                l.yBotS[i] = f.yBotS[i];
+            }
+            for (int k = 0; k < 8; ++k) {
+                l.xM[k] = f.xM[k];
+                l.xT[k] = f.xT[k];
+            }
             l.dbg = h->debugFlags;
             l.prefetch = h->prefetch;
             int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);

@@ -87,26 +87,6 @@ __device__ __forceinline__ int exact_div(int n, int d)
     return ((n ^ d) < 0) ? -static_cast<int>(q) : static_cast<int>(q);
 }
 
-// Fast exact truncating division for the streamer's border paths.  Precondition (holds there):
-// |n| < 2^24 or |d| >= 64, and |n / d| < 2^22 -- then the float estimate is within 1 of the
-// true quotient, and two branch-free correction steps each way make it exact.
-__device__ __forceinline__ int exact_div_fast(int n, int d)
-{
-    const uint32_t an = n < 0 ? 0u - static_cast<uint32_t>(n) : static_cast<uint32_t>(n);
-    const uint32_t ad = d < 0 ? 0u - static_cast<uint32_t>(d) : static_cast<uint32_t>(d);
-    const float r = __builtin_amdgcn_rcpf(static_cast<float>(ad));
-    uint32_t q = static_cast<uint32_t>(static_cast<float>(an) * r);
-    int rem = static_cast<int>(an - q * ad);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const bool lo = rem < 0, hi = rem >= static_cast<int>(ad);
-        q = lo ? q - 1 : (hi ? q + 1 : q);
-        rem = lo ? rem + static_cast<int>(ad) : (hi ? rem - static_cast<int>(ad) : rem);
-    }
-    const int sq = ((n ^ d) < 0) ? -static_cast<int>(q) : static_cast<int>(q);
-    return d == 0 ? 0 : sq;
-}
-
 __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 
 // A value the instruction combiner cannot see through.  Used on clamped bytes before packing:
@@ -255,15 +235,26 @@ __global__ __launch_bounds__(256) void general_kernel(GeneralArgs a)
 
 // ================================================================ Lanczos row-band streamer
 //
-// Workgroup = one row band of one frame, spanning the full source width: thread t owns source
-// columns [16t, 16t+16).  It walks the band's output rows top to bottom holding the NY source
-// rows of the vertical window in registers (unpacked to u16 pairs, a static ring: every source
-// row is fetched from HBM once per band with coalesced 16-B loads and unpacked once), prefetching
-// the next KY rows while it computes.  The vertical result (the reference's int16 work row) goes
-// to a double-buffered LDS row with zero pads, so the horizontal taps -- including the masked
-// border columns, whose invalid taps then read zero -- come from LDS with aligned 16-B reads.
-// Border rows/columns differ from the interior only by a per-row / per-column divisor
-// (renormalisation), applied where the reference applies it.
+// One WAVE = one row band of one frame x one strip of output columns; waves are independent (no
+// LDS, no barriers).  Lane l of a wave owns the 16 source columns [cb, cb + 16), cb = KX*x0 - 16
+// + 16*l, and (lanes 1..62) produces the 16/KX output columns that start at x0 + (l-1)*16/KX.
+// The wave walks its band's output rows top to bottom; each source row is fetched from HBM once
+// per band with coalesced 16-B buffer loads (off-image rows/columns lie outside the buffer
+// range and read as zero -- exactly the masked border sums of the reference), unpacked to u16
+// pairs, and multiplied into the P = NY/KY output rows that still need it (accumulator ring).
+// The vertical sum is the reference's int16 work row; the horizontal taps read it from the
+// lane itself and its neighbours (DPP row shifts), then two packed saturating shifts produce the
+// output bytes.
+//
+// Control flow is straight-line: the row loop is unrolled by LV = lcm(P, PD) so every ring slot
+// and prefetch slot is a static register (no phase dispatch, no loop-carried register shuffles),
+// and only uniform branches remain (priming rows, band end, border rows, edge waves).
+//
+// Border rows / columns differ from the interior only by a divisor (renormalisation, the
+// reference's resizeYborder :487-489 and resizeXborder :572); both are exact multiply-high
+// divisions with host-computed constants (plan.cpp magic_y / magic_x).  The last wave of a row
+// is aligned to the right image edge (it may overlap its neighbour; overlapping bytes are equal)
+// so the at most 4 border columns per side sit at static positions of one lane.
 
 struct LanczosArgs {
     LanczosDev l;
@@ -272,10 +263,36 @@ struct LanczosArgs {
     int srcBytes, dstBytes;  // extent of one frame's source window / destination band (buffer range)
     int bands, wavesPerRow;  // wave grid per frame: band-major, column-minor
     int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
-                             // 2 = no prefetch loads, 4 = no barrier.  0 in production.
+                             // 2 = no source loads.  0 in production.
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+// (sat_u8(a >> 20), sat_u8(b >> 20)) into bits 0..15 of the result (bits 16..31 undefined) /
+// into bits 16..31 of w (bits 0..15 kept).  gfx950 v_ashr_pk_u8_i32: src0 -> byte 0, src1 ->
+// byte 1, the other half of the destination is preserved (probed on MI355X,
+// scripts/ubench/pk_test.hip).
+__device__ __forceinline__ uint32_t pack_lo(int a, int b)
+{
+    uint32_t w;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 20" : "=v"(w) : "v"(a), "v"(b));
+    return w;
+}
+__device__ __forceinline__ uint32_t pack_hi(uint32_t w, int a, int b)
+{
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 20 op_sel:[0,0,0,1]" : "+v"(w) : "v"(a), "v"(b));
+    return w;
+}
+
+// int16(n * 64 / deno) for both int16 halves of w (C truncation), deno via (m, s) of magic_y.
+__device__ __forceinline__ uint32_t ydiv2(uint32_t w, uint32_t m, int s)
+{
+    const int lo = static_cast<int16_t>(w & 0xffffu), hi = static_cast<int16_t>(w >> 16);
+    const uint32_t qlo = __umulhi(static_cast<uint32_t>(lo < 0 ? -lo : lo) << s, m);
+    const uint32_t qhi = __umulhi(static_cast<uint32_t>(hi < 0 ? -hi : hi) << s, m);
+    const uint32_t rlo = lo < 0 ? 0u - qlo : qlo, rhi = hi < 0 ? 0u - qhi : qhi;
+    return __builtin_amdgcn_perm(rhi, rlo, 0x05040100u);  // (rlo.lo16, rhi.lo16)
+}
 
 template <int KY, int KX, int NY, int NXP, int OFFXD, int PD>
 __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
@@ -284,15 +301,18 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
     constexpr int OPW = 62 * OUTS;           // outputs per wave (lanes 1..62)
     constexpr int P = NY / KY;               // output rows pending at once (accumulator ring)
     static_assert(NY % KY == 0, "NY must be a multiple of KY");
-    constexpr int LV = P * PD / cgcd(P, PD);  // static variants: accumulator slot x prefetch slot
+    constexpr int LV = P * PD / cgcd(P, PD);  // unroll: accumulator slot x prefetch slot
     constexpr int DLO = OFFXD;               // first work dword a lane reads, relative to its own
     constexpr int DHI = (OUTS - 1) * KX / 2 + OFFXD + NXP / 2;  // one past the last
     static_assert(DLO >= -8 && DHI <= 16, "horizontal taps must stay within the neighbouring lanes");
-    static_assert(OUTS == 8 || OUTS == 4, "");
+    static_assert(OUTS == 8, "edge handling assumes 8 outputs per lane (KX == 2)");
 
     const LanczosDev &L = a.l;
     const int lane = static_cast<int>(threadIdx.x) & 63;
-    const int wib = static_cast<int>(threadIdx.x) >> 6;  // wave in block
+    // wave in block, made provably wave-uniform: otherwise everything derived from it (band,
+    // rows, the row counter) is treated as divergent -- row offsets land in VGPRs, every buffer
+    // load becomes a readfirstlane loop and row branches become exec-mask branches
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const int g = static_cast<int>(blockIdx.x) * 4 + wib;  // wave index in the (band, column) grid
     if (g >= a.bands * a.wavesPerRow)
         return;  // whole wave: nothing below synchronises across waves
@@ -302,18 +322,14 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
     if (y0 >= y1)
         return;
 
-    // per-wave copy of the border divisors (read with per-lane indices; LDS keeps them off the
-    // VMEM counter); only this wave touches its copy, so no barrier is needed
-    __shared__ int btabs[4][64];
-    int *btab = btabs[wib];
-    btab[lane] = L.border[lane];
-
-    const int x0 = wcol * OPW;                    // first output column of lane 1
+    // first output column of lane 1; the last wave is aligned to the right edge (dstW % 8 == 0)
+    const int x0 = max(0, min(wcol * OPW, L.dstW - OPW));
     const int cb = KX * x0 - 16 + 16 * lane;      // first source column of this lane's block
     const int outX = x0 + (lane - 1) * OUTS;      // first output column of this lane
     const bool produce = lane >= 1 && lane <= 62 && outX < L.dstW;
     const int voff = (cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;  // off-image blocks read zero
-    (void)outX;
+    const bool edgeL = x0 == 0, edgeR = x0 + OPW >= L.dstW;       // wave holds border columns
+    const bool laneL = outX == 0, laneR = outX == L.dstW - OUTS;  // ... in this lane
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
@@ -323,20 +339,19 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0;
     const int dbg = a.dbg;
+    const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
+    const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;  // dropped for non-producers
 
-    // Branch-free row load: rows outside the image (r < 0 wraps to a huge unsigned soffset,
-    // r >= srcH lies past the range) and off-image column blocks are outside the descriptor's
-    // range and read as zero -- exactly the masked border sums.  No branches keep the waitcnt
-    // counting exact, so the next rows' prefetch stays in flight across the whole row.
+    // Branch-free row load (r < 0 wraps to a huge unsigned soffset, r >= srcH lies past the
+    // range): no branches keep the waitcnt counting exact across the unrolled rows.
     auto load_row = [&](int r) -> uint4 {
-        u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, (dbg & 2) ? 0x7ff00000 : voff, (r - srcRow0) * srcSt,
-                                                        2 /* nt */);
+        u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, (r - srcRow0) * srcSt, 2 /* nt */);
         return make_uint4(q.x, q.y, q.z, q.w);
     };
 
-    // Accumulator ring: each source row, as it arrives, is multiplied into the partial sums of
-    // the P output rows that still need it (tap NY-KY*(q+1)+j for the q-th pending row).  Row
-    // yy completes in slot yy mod P.  Iterations start P-1 rows early to prime the ring.
+    // Accumulator ring: a source row is multiplied into the partial sums of the P output rows
+    // that still need it (tap NY-KY*(q+1)+j for the q-th pending row); row yy completes in slot
+    // (yy - yStart) mod P.  Iterations start P-1 rows early to prime the ring.
     uint32_t accR[P][8];
 #pragma unroll
     for (int q = 0; q < P; ++q)
@@ -344,136 +359,100 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
         for (int c = 0; c < 8; ++c)
             accR[q][c] = 0;
     const int yStart = y0 - (P - 1);
-    // prefetch ring: the source rows of iteration `it` live in slot it % PD; they are issued PD
-    // iterations ahead (static slots: moving a register with a load in flight would force a wait)
+    // prefetch ring: the KY new source rows of iteration i live in slot i % PD, issued PD
+    // iterations ahead
     uint4 pre[PD][KY];
 #pragma unroll
     for (int i = 0; i < PD; ++i)
 #pragma unroll
         for (int j = 0; j < KY; ++j)
             pre[i][j] = load_row(KY * (yStart + i) + L.offY + NY - KY + j);
-    {
-        // Dropped store (out of range): makes the prologue end in the same VMEM pattern as the
-        // loop back-edge (loads, then one store) so waits for `pre` stay counted, not vmcnt(0).
-        u32x2 z = {0u, 0u};
-        __builtin_amdgcn_raw_buffer_store_b64(z, dstR, 0x7ff00000, 0, 0);
-    }
 
-    int phase = 0;  // == (yy - yStart) mod LV; row yy completes in accumulator slot phase % P
-    for (int yy = yStart; yy < y1; ++yy) {
-        uint32_t acc[8];
-        // ---- ring-dependent part, one static variant per phase (uniform branch)
+    for (int base = yStart; base < y1; base += LV) {
         static_for<LV>([&](auto uc) {
             constexpr int v = decltype(uc)::value;
-            constexpr int u = v % P;   // accumulator slot of row yy
-            constexpr int ps = v % PD; // prefetch slot holding row yy's new source rows
-            if (phase == v) {
-                uint32_t nw[KY][8];
+            constexpr int u = v % P;   // accumulator slot completing at this row
+            constexpr int ps = v % PD; // prefetch slot holding this row's new source rows
+            const int yy = base + v;
+            uint32_t nw[KY][8];
 #pragma unroll
-                for (int j = 0; j < KY; ++j)
-                    unpack16(pre[ps][j], nw[j]);
+            for (int j = 0; j < KY; ++j)
+                unpack16(pre[ps][j], nw[j]);
 #pragma unroll
-                for (int j = 0; j < KY; ++j)  // (past the band end this reads unused rows)
-                    pre[ps][j] = load_row(KY * (yy + PD) + L.offY + NY - KY + j);
-                // vertical taps: int16 wrap == low half of the packed u16 MAD.  The q loop is
-                // inside the column loop's outer level so the 8 independent column chains stay
-                // interleaved (gfx950 wants ~9 wait states between DEPENDENT v_pk_mad_u16).
+            for (int j = 0; j < KY; ++j)  // (rows past the band end are loaded and unused)
+                pre[ps][j] = load_row(KY * (yy + PD) + L.offY + NY - KY + j);
+            // vertical taps: int16 wrap == low half of the packed u16 MAD; tap-outer so the 8
+            // independent column chains interleave (dependent v_pk_mad_u16 need ~9 wait states)
 #pragma unroll
-                for (int q = 0; q < P; ++q) {
-                    constexpr int dummy = 0;
-                    (void)dummy;
+            for (int q = 0; q < P; ++q)
 #pragma unroll
-                    for (int j = 0; j < KY; ++j) {
-                        const uint32_t cq = L.cy[NY - KY * (q + 1) + j];
-                        uint32_t *ar = accR[(u + q) % P];
+                for (int j = 0; j < KY; ++j) {
+                    const uint32_t cq = L.cy[NY - KY * (q + 1) + j];
+                    uint32_t *ar = accR[(u + q) % P];
 #pragma unroll
-                        for (int c = 0; c < 8; ++c)
-                            ar[c] = (q == P - 1 && j == 0) ? pk_mul(nw[j][c], cq) : pk_mad(nw[j][c], cq, ar[c]);
-                    }
+                    for (int c = 0; c < 8; ++c)
+                        ar[c] = (q == P - 1 && j == 0) ? pk_mul(nw[j][c], cq) : pk_mad(nw[j][c], cq, ar[c]);
                 }
+            if (yy < y0 || yy >= y1)
+                return;  // priming row / past the band end (uniform)
+
+            uint32_t acc[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c] = accR[u][c];
+            if (yy < L.mainBeginY || yy >= L.mainEndY) {
+                // border row (uniform, rare): work = int16(int(nume) * 64 / deno); invalid rows
+                // were read as zero, so nume is already the masked sum
+                const bool top = yy < L.mainBeginY;
+                const int bi = top ? yy : yy - L.mainEndY;
+                const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
+                const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
 #pragma unroll
                 for (int c = 0; c < 8; ++c)
-                    acc[c] = accR[u][c];
-                // distinct per phase: stops the compiler from tail-merging the P structurally
-                // identical variants into one block fed by register shuffles (seen: scratch spills)
-                asm volatile("; ring phase %0" ::"n"(v));
+                    acc[c] = ydiv2(acc[c], m, sh);
             }
-        });
-        phase = phase + 1 == LV ? 0 : phase + 1;
-        if (yy < y0)
-            continue;  // priming iterations (uniform)
 
-        if (yy < L.mainBeginY || yy >= L.mainEndY) {
-            // border row (uniform, rare): work = int16(int(nume) * 64 / deno) (resizeYborder
-            // :487-489); invalid rows were read as zero, so nume is already the masked sum.
-            const int den = yy < L.mainBeginY ? btab[yy] : btab[16 + yy - L.mainEndY];
+            // neighbour work columns by DPP (lane l-1 / l+1), then the horizontal taps
+            uint32_t d[DHI - DLO];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const int lo = exact_div_fast(static_cast<int>(static_cast<int16_t>(acc[c] & 0xffffu)) * 64, den);
-                const int hi = exact_div_fast(static_cast<int>(static_cast<int16_t>(acc[c] >> 16)) * 64, den);
-                acc[c] = (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
+            for (int j = DLO; j < DHI; ++j) {
+                if (j < 0)
+                    d[j - DLO] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                        0, static_cast<int>(acc[8 + j]), 0x138 /* wave_shr:1 */, 0xf, 0xf, false));
+                else if (j >= 8)
+                    d[j - DLO] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                        0, static_cast<int>(acc[j - 8]), 0x130 /* wave_shl:1 */, 0xf, 0xf, false));
+                else
+                    d[j - DLO] = acc[j];
             }
-        }
-
-        // ---- neighbour work columns by DPP (lane l-1 / l+1), then horizontal taps
-        uint32_t d[DHI - DLO];
-#pragma unroll
-        for (int j = DLO; j < DHI; ++j) {
-            if (j < 0)
-                d[j - DLO] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc[8 + j]),
-                                                                               0x138 /* wave_shr:1 */, 0xf, 0xf, false));
-            else if (j >= 8)
-                d[j - DLO] = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(acc[j - 8]),
-                                                                               0x130 /* wave_shl:1 */, 0xf, 0xf, false));
-            else
-                d[j - DLO] = acc[j];
-        }
-        int sum[OUTS];
-#pragma unroll
-        for (int k = 0; k < OUTS; ++k) {
-            int s = 1 << 19;
-#pragma unroll
-            for (int p = 0; p < NXP / 2; ++p)
-                s = sdot2(d[(KX * k) / 2 + OFFXD - DLO + p], L.cx[p], s);
-            sum[k] = s;
-        }
-        int val[OUTS];
-#pragma unroll
-        for (int k = 0; k < OUTS; ++k)
-            val[k] = sum[k] >> 20;
-        if (produce && (outX < L.mainBeginX || outX + OUTS > L.mainEndX)) {
-            // border columns (edge lanes only): int16((nume + 2^19) / (deno * 64)),
-            // resizeXborder :572.  The dot product above already IS nume + 2^19 (off-image
-            // taps read zero); only the divisor differs.
+            int sum[OUTS];
 #pragma unroll
             for (int k = 0; k < OUTS; ++k) {
-                const int x = outX + k;
-                if (x < L.mainBeginX)
-                    val[k] = exact_div_fast(sum[k], btab[32 + x]);
-                else if (x >= L.mainEndX)
-                    val[k] = exact_div_fast(sum[k], btab[48 + x - L.mainEndX]);
-            }
-        }
-        uint32_t ow[OUTS / 4];
+                int sacc = 1 << 19;
 #pragma unroll
-        for (int k4 = 0; k4 < OUTS / 4; ++k4) {
-            uint32_t word = 0;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                word |= opaque(static_cast<uint32_t>(clamp255(static_cast<int16_t>(val[4 * k4 + kk])))) << (8 * kk);
-            ow[k4] = word;
-        }
-        {
-            // unconditional store; non-producing lanes aim past the range and are dropped
-            const int so = (yy - a.io.dstRow0) * dstSt;
-            const int vo = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
-            if constexpr (OUTS == 8) {
-                u32x2 o = {ow[0], ow[1]};
-                __builtin_amdgcn_raw_buffer_store_b64(o, dstR, vo, so, 0);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b32(ow[0], dstR, vo, so, 0);
+                for (int p = 0; p < NXP / 2; ++p)
+                    sacc = sdot2(d[(KX * k) / 2 + OFFXD - DLO + p], L.cx[p], sacc);
+                sum[k] = sacc;
             }
-        }
+            if (edgeL || edgeR) {
+                // edge wave (uniform): values k < 4 of the left edge lane / k >= 4 of the right
+                // edge lane become floor(max(sum, 0) / D) -- negative border quotients clamp to
+                // 0 like the reference's int16 -> u8 clamp -- re-scaled by 2^20 for the pack
+#pragma unroll
+                for (int k = 0; k < OUTS; ++k) {
+                    const bool side = k < 4 ? edgeL : edgeR;
+                    if (side) {
+                        const uint32_t n = static_cast<uint32_t>(max(sum[k], 0));
+                        const uint32_t q = __umulhi(n, L.xM[k]) >> L.xT[k];
+                        sum[k] = (k < 4 ? laneL : laneR) ? static_cast<int>(q << 20) : sum[k];
+                    }
+                }
+            }
+            u32x2 o;
+            o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+            o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        });
     }
 }
 

@@ -38,7 +38,10 @@ struct LanczosDev {
     uint32_t cy[16];             // (c, c) u16 pairs
     uint32_t cx[16];             // (c_2p, c_2p+1) int16 pairs
     int mainBeginY, mainEndY, mainBeginX, mainEndX;
-    const int *border;           // device: [0,16) denoYTop, [16,32) denoYBot, [32,48) dXLeft, [48,64) dXRight
+    // exact border divisions by multiply-high (plan.hpp FastLanczos): kernel arguments, so they
+    // arrive in SGPRs and cost no device table
+    uint32_t yTopM[16], yBotM[16], xM[8];
+    int yTopS[16], yBotS[16], xT[8];
     int dbg;                     // timing experiments only (see kernels.hip)
     int prefetch;                // prefetch depth in output rows (1..3)
 };

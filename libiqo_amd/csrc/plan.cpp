@@ -366,6 +366,56 @@ void coords_linear(AxisPlan *a)
 
 // ---------------------------------------------------------------- fast-path eligibility
 
+int ceil_log2(uint64_t d)
+{
+    int l = 0;
+    while ((uint64_t(1) << l) < d)
+        ++l;
+    return l;
+}
+
+} // namespace
+
+// Granlund & Montgomery (PLDI'94) Thm 4.2: with 2^(N+l) <= m*d <= 2^(N+l) + 2^l,
+// floor(n / d) == floor(m * n / 2^(N+l)) for all 0 <= n < 2^N.  m = ceil(2^(N+l) / d) with
+// l = ceil(log2 d) satisfies it.
+//
+// Y border rows: n = |nume| * 64 < 2^22 (nume is int16), N = 22, d = deno in [1, 1024] (l <= 10):
+// floor(m * n / 2^(22+l)) == umulhi(n << (10 - l), m) == umulhi(|nume| << (16 - l), m).
+bool magic_y(int32_t deno, uint32_t *m, int32_t *s)
+{
+    if (deno < 1 || deno > 1024)
+        return false;
+    const int l = ceil_log2(static_cast<uint64_t>(deno));
+    const uint64_t k = 22 + static_cast<uint64_t>(l);
+    const uint64_t mm = ((uint64_t(1) << k) + static_cast<uint64_t>(deno) - 1) / static_cast<uint64_t>(deno);
+    if (mm >= (uint64_t(1) << 32))
+        return false;
+    *m = static_cast<uint32_t>(mm);
+    *s = 16 - l;
+    return true;
+}
+
+// X edge values: n = X sum clamped at 0, n < 2^31, N = 31, d = 64 * deno (>= 2):
+// floor(m * n / 2^(31+l)) == umulhi(n, m) >> (l - 1), m < 2^32 because d > 2^(l-1).
+bool magic_x(int64_t d, uint32_t *m, int32_t *t)
+{
+    if (d < 2 || d > (int64_t(1) << 31))
+        return false;
+    const int l = ceil_log2(static_cast<uint64_t>(d));
+    const uint64_t k = 31 + static_cast<uint64_t>(l);
+    if (k >= 64)
+        return false;
+    const uint64_t mm = ((uint64_t(1) << k) + static_cast<uint64_t>(d) - 1) / static_cast<uint64_t>(d);
+    if (mm >= (uint64_t(1) << 32))
+        return false;
+    *m = static_cast<uint32_t>(mm);
+    *t = l - 1;
+    return true;
+}
+
+namespace {
+
 void pick_fast_lanczos(Plan *p)
 {
     AxisPlan &x = p->x, &y = p->y;
@@ -422,6 +472,38 @@ void pick_fast_lanczos(Plan *p)
         f.dXLeft.push_back(64 * x.coord[c].aux);
     for (int c = x.mainEnd; c < p->dstW; ++c)
         f.dXRight.push_back(64 * x.coord[c].aux);
+    // Streamer arithmetic preconditions (kernels.hip, lanczos_stream_kernel):
+    //  * the int32 X sum never overflows and (sum >> 20) fits int16 for ANY int16 work values, so
+    //    the packed saturating shift (v_ashr_pk_u8_i32) equals clamp255(int16(sum >> 20));
+    //  * border divisions use the exact multiply-high forms of magic_y / magic_x;
+    //  * output width multiple of 8 and <= 4 border columns per side: the last wave is aligned
+    //    to the right edge, so border columns sit at static positions of the edge lanes.
+    int64_t sabs = 0;
+    for (int16_t c : f.cx)
+        sabs += c < 0 ? -c : c;
+    const int64_t maxSum = 32768 * sabs + (1 << 19);
+    if (maxSum >= (int64_t(1) << 31) || (maxSum >> 20) >= 32768)
+        return;
+    if (p->dstW % 8 || x.mainBegin > 4 || p->dstW - x.mainEnd > 4 || y.mainBegin > 16 || p->dstH - y.mainEnd > 16)
+        return;
+    for (size_t i = 0; i < f.denoYTop.size(); ++i)
+        if (!magic_y(f.denoYTop[i], &f.yTopM[i], &f.yTopS[i]))
+            return;
+    for (size_t i = 0; i < f.denoYBot.size(); ++i)
+        if (!magic_y(f.denoYBot[i], &f.yBotM[i], &f.yBotS[i]))
+            return;
+    for (int k = 0; k < 8; ++k) {
+        const int c = k < 4 ? k : p->dstW - 8 + k;  // column of edge-lane value k
+        int64_t D = int64_t(1) << 20;               // identity: floor(s / 2^20) == s >> 20
+        if (k < 4 && c < x.mainBegin)
+            D = f.dXLeft[static_cast<size_t>(c)];
+        else if (k >= 4 && c >= x.mainEnd && c >= 0)
+            D = f.dXRight[static_cast<size_t>(c - x.mainEnd)];
+        if (D != (int64_t(1) << 20) && (maxSum / D >= 32768))
+            return;  // border quotient must fit int16 (it is int16-cast before the clamp)
+        if (!magic_x(D, &f.xM[k], &f.xT[k]))
+            return;
+    }
     // instantiated shapes (kernels.hip): (KY,KX,NY,NXP,offX/2) = (2,2,10,14,-3) Lanczos-3 2:1,
     // (2,2,8,10,-2) Lanczos-2 2:1.  Everything else runs the general kernel.
     bool inst = KY == 2 && KX == 2 && ((f.NY == 10 && f.NXP == 14 && f.offX == -6) ||

@@ -58,7 +58,19 @@ struct FastLanczos {
     int mainBeginY = 0, mainEndY = 0, mainBeginX = 0, mainEndX = 0;
     std::vector<int32_t> denoYTop, denoYBot; // wrapped int16 valid-tap sums per border row
     std::vector<int32_t> dXLeft, dXRight;    // 64 * valid-tap sum per border column
+    // Exact division by multiply-high (Granlund-Montgomery), see magic_y / magic_x in plan.cpp.
+    // Y border row r: int16(n * 64 / deno) = sign(n) * umulhi(|n| << yS, yM)      (|n| <= 2^15)
+    // X edge value k (k < 4: columns k of the left edge lane; k >= 4: columns dstW - 8 + k of the
+    // right edge lane): floor(s / D) = umulhi(s, xM) >> xT for 0 <= s < 2^31 (identity magic,
+    // D = 2^20, for columns of those lanes that are not border columns).
+    uint32_t yTopM[16] = {}, yBotM[16] = {}, xM[8] = {};
+    int32_t yTopS[16] = {}, yBotS[16] = {}, xT[8] = {};
 };
+
+// Exact-division constants (exposed for tests): false if the divisor is outside the range the
+// streamer's formulas are proven for.
+bool magic_y(int32_t deno, uint32_t *m, int32_t *s);
+bool magic_x(int64_t d, uint32_t *m, int32_t *t);
 
 struct FastArea {
     int KY = 0, KX = 0;
