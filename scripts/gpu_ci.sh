@@ -12,7 +12,7 @@ want() { [[ " $* " == *" all "* ]] || [[ " $ARGS " == *" $1 "* ]]; }
 ARGS="$*"
 [ -z "$ARGS" ] && ARGS="tests bench"
 if want tests; then
-  timeout -k 10 600 python -m pytest tests -m gpu -q -x > "$OUT/pytest_gpu.log" 2>&1 || { echo "pytest failed"; tail -20 "$OUT/pytest_gpu.log"; exit 1; }
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 || { echo "pytest failed"; tail -20 "$OUT/pytest_gpu.log"; exit 1; }
   tail -1 "$OUT/pytest_gpu.log"
 fi
 if want bench; then
