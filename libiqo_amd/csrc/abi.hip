@@ -33,6 +33,8 @@ struct iqo_hip_plan {
     int bands = 0;
     int debugFlags = 0;
     int prefetch = 3;  // best of the 1/2/3 sweep on C2 (straight-line streamer)
+    int streamVariant = 0;  // 0: symmetric streamer where eligible, 1: accumulator-ring streamer
+    int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     hipStream_t stream = nullptr;
     uint8_t *stageSrc = nullptr, *stageDst = nullptr;
     size_t stageSrcCap = 0, stageDstCap = 0;
@@ -279,6 +281,12 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             }
             l.dbg = h->debugFlags;
             l.prefetch = h->prefetch;
+            l.sym = f.sym && h->streamVariant != 1 ? 1 : 0;
+            l.NX = f.NX;
+            l.offXO = f.offXO;
+            for (int i = 0; i < f.NX / 2 && i < 8; ++i)
+                l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
+            l.np = h->lanes;
             int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
             e = iqo_amd::launch_lanczos_stream(l, io, rb, re, bands, s);
         } else if (kernel == IQO_KERNEL_AREA_INT) {
@@ -400,6 +408,18 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 1 || value > 3)
             return IQO_HIP_EINVAL;
         h->prefetch = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric (default), 1 ring
+        if (value < 0 || value > 1)
+            return IQO_HIP_EINVAL;
+        h->streamVariant = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "lanes")) {  // symmetric streamer producing lanes per wave (0 = auto)
+        if (value < 0 || value > 62)
+            return IQO_HIP_EINVAL;
+        h->lanes = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "bands")) {

@@ -264,6 +264,7 @@ struct LanczosArgs {
     int bands, wavesPerRow;  // wave grid per frame: band-major, column-minor
     int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
                              // 2 = no source loads.  0 in production.
+    int np;                  // producing lanes per wave (symmetric streamer)
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -445,6 +446,191 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
                         const uint32_t n = static_cast<uint32_t>(max(sum[k], 0));
                         const uint32_t q = __umulhi(n, L.xM[k]) >> L.xT[k];
                         sum[k] = (k < 4 ? laneL : laneR) ? static_cast<int>(q << 20) : sum[k];
+                    }
+                }
+            }
+            u32x2 o;
+            o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+            o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        });
+    }
+}
+
+// ================================================================ symmetric Lanczos streamer
+//
+// Same wave geometry and border handling as the ring streamer above, but the arithmetic is laid
+// out for gfx950's issue rates (scripts/ubench/isa_rate*.hip on MI355X): VOP2 adds and logic ops
+// issue in 2 cycles per wave, while v_pk_mad_u16, v_dot2*, v_perm and DPP moves take 4.
+//
+//  * Vertical: the 2:1 Lanczos Y table is symmetric (c_i == c_{NY-1-i}), so the work value is
+//    sum_{p < NY/2} c_p * (s[top+p] + s[top+NY-1-p]).  The pair sums of unpacked u16 bytes are
+//    <= 510 per half, so one full-rate v_add_u32 adds both halves; then one v_pk_mad_u16 per pair
+//    (its low 16 bits per half ARE the reference's int16 wrap: the sum is taken mod 2^16 in any
+//    order).  NY/2 adds + NY/2 packed MACs per column pair instead of NY packed MACs.  This needs
+//    all NY source rows of an output row at once: a register WINDOW of NY unpacked rows (8 u16
+//    pairs per lane each), refilled with two rows per output row.
+//  * Horizontal: bytes are unpacked into ODD-aligned pairs Q_j = (cb+2j-1, cb+2j) (the lane's
+//    own pairs j = 1..8; byte cb+16 comes from the right neighbour by DPP).  The taps of output
+//    x start at the odd column 2x + offXO, so each output is exactly NX/2 v_dot2_i32_i16 on
+//    Q_{k+p+JLO} with no zero padding.
+//  * The first dot of every output takes the rounding bias from a VGPR (VOP3P form), and the
+//    DPP neighbour moves use bound_ctrl, so neither needs an initialising move.
+//  * A wave has np producing lanes (1..np) and halo lanes 0 and np+1; the host sizes np so the
+//    waves of a row tile the output width exactly when it can (1920 = 4 x 60 x 8).  Idle lanes
+//    (> np+1) load nothing (out-of-range offsets) and store nothing.
+//  * Rows past the band's last needed source row are loaded out of range (no HBM traffic).
+
+template <int NY, int NX, int OFFX, int PD, bool C0ONE>
+__global__ __launch_bounds__(256, 3) void lanczos_sym_kernel(LanczosArgs a)
+{
+    constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
+    static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
+    constexpr int LV = H * PD / cgcd(H, PD);    // unroll: window slot x prefetch slot
+    constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
+    constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
+    static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
+
+    const LanczosDev &L = a.l;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const int g = static_cast<int>(blockIdx.x) * 4 + wib;
+    if (g >= a.bands * a.wavesPerRow)
+        return;
+    const int band = g / a.wavesPerRow, wcol = g - band * a.wavesPerRow;
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+
+    const int np = a.np, opw = 8 * np;
+    const int x0 = max(0, min(wcol * opw, L.dstW - opw));
+    const int cb = 2 * x0 - 16 + 16 * lane;
+    const int outX = x0 + (lane - 1) * 8;
+    const bool produce = lane >= 1 && lane <= np && outX < L.dstW;
+    const int voff = (lane <= np + 1 && cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;
+    const bool edgeL = x0 == 0, edgeR = x0 + opw >= L.dstW;
+    const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0;
+    const int dbg = a.dbg;
+    const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
+    const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
+    // last source row the band reads: rows beyond it (prefetch overrun) are loaded out of range
+    const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;
+    const uint32_t bias = opaque(1u << 19);  // rounding bias in a VGPR (VOP3P src2 of the first dot)
+
+    auto load_row = [&](int r) -> uint4 {
+        const int so = r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000;
+        u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, so, 2 /* nt */);
+        return make_uint4(q.x, q.y, q.z, q.w);
+    };
+    // odd-aligned u16 pairs Q_1..Q_8 of one row: (b1,b2) (b3,b4) ... (b15, b16), b16 = right
+    // neighbour's byte 0
+    auto unpack_odd = [&](uint4 v, uint32_t (&q)[8]) {
+        const uint32_t r = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v.x), 0x130 /* wave_shl:1 */,
+                                                                          0xf, 0xf, true));
+        q[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c020c01u);
+        q[1] = __builtin_amdgcn_perm(v.y, v.x, 0x0c040c03u);
+        q[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c020c01u);
+        q[3] = __builtin_amdgcn_perm(v.z, v.y, 0x0c040c03u);
+        q[4] = __builtin_amdgcn_perm(0u, v.z, 0x0c020c01u);
+        q[5] = __builtin_amdgcn_perm(v.w, v.z, 0x0c040c03u);
+        q[6] = __builtin_amdgcn_perm(0u, v.w, 0x0c020c01u);
+        q[7] = __builtin_amdgcn_perm(r, v.w, 0x0c040c03u);
+    };
+
+    // window: at output row i the NY source rows rowBase + 2(i - y0) + t (t < NY) live in
+    // slots (2(i - y0) + t) mod NY; iteration i brings the last two (t = NY-2, NY-1)
+    uint32_t win[NY][8];
+    const int iStart = y0;
+    const int rowBase = 2 * y0 + L.offY;  // first source row of output row y0
+    uint4 pre[PD][2];
+#pragma unroll
+    for (int i = 0; i < PD; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            pre[i][j] = load_row(rowBase + 2 * i + NY - 2 + j);
+    // rows rowBase .. rowBase + NY - 3 (window slots 0 .. NY-3) before the first iteration
+#pragma unroll
+    for (int t = 0; t < NY - 2; ++t)
+        unpack_odd(load_row(rowBase + t), win[t]);
+
+    for (int base = iStart; base < y1; base += LV) {
+        static_for<LV>([&](auto uc) {
+            constexpr int v = decltype(uc)::value;
+            constexpr int ps = v % PD;
+            const int yy = base + v;
+            // the two new rows of this iteration -> window slots (2v + NY - 2) mod NY, +1
+            unpack_odd(pre[ps][0], win[(2 * v + NY - 2) % NY]);
+            unpack_odd(pre[ps][1], win[(2 * v + NY - 1) % NY]);
+            const int rNext = rowBase + 2 * (yy + PD - iStart) + NY - 2;
+            pre[ps][0] = load_row(rNext);
+            pre[ps][1] = load_row(rNext + 1);
+            if (yy >= y1)
+                return;  // past the band end (uniform)
+
+            // vertical: pair p = slots (2v + p, 2v + NY - 1 - p) mod NY
+            uint32_t acc[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t p0 = win[(2 * v) % NY][c] + win[(2 * v + NY - 1) % NY][c];
+                acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
+            }
+#pragma unroll
+            for (int p = 1; p < H; ++p)
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
+                    acc[c] = pk_mad(pp, L.cy[p], acc[c]);
+                }
+            if (yy < L.mainBeginY || yy >= L.mainEndY) {
+                // border row (uniform, rare): rows outside the image were read as zero
+                const bool top = yy < L.mainBeginY;
+                const int bi = top ? yy : yy - L.mainEndY;
+                const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
+                const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
+#pragma unroll
+                for (int c = 0; c < 8; ++c)
+                    acc[c] = ydiv2(acc[c], m, sh);
+            }
+
+            // Q_j for j in [JLO, JHI): own pairs 1..8, neighbours' by DPP
+            uint32_t q[JHI - JLO];
+#pragma unroll
+            for (int j = JLO; j < JHI; ++j) {
+                if (j <= 0)
+                    q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
+                        static_cast<int>(acc[j + 7]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+                else if (j >= 9)
+                    q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
+                        static_cast<int>(acc[j - 9]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+                else
+                    q[j - JLO] = acc[j - 1];
+            }
+            int sum[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                int sacc = sdot2(q[k], L.cxo[0], static_cast<int>(bias));
+#pragma unroll
+                for (int p = 1; p < NX / 2; ++p)
+                    sacc = sdot2(q[k + p], L.cxo[p], sacc);
+                sum[k] = sacc;
+            }
+            if (edgeL || edgeR) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const bool side = k < 4 ? edgeL : edgeR;
+                    if (side) {
+                        const uint32_t n = static_cast<uint32_t>(max(sum[k], 0));
+                        const uint32_t qq = __umulhi(n, L.xM[k]) >> L.xT[k];
+                        sum[k] = (k < 4 ? laneL : laneR) ? static_cast<int>(qq << 20) : sum[k];
                     }
                 }
             }
@@ -643,9 +829,20 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     bands = max(1, min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
-    const int opw = 62 * (16 / l.KX);
-    const int wpr = (l.dstW + opw - 1) / opw;
-    LanczosArgs a{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg};
+    int opw = 62 * (16 / l.KX);
+    int wpr = (l.dstW + opw - 1) / opw;
+    int np = 62;
+    if (l.sym) {
+        // producing lanes per wave: the fewest waves per row, then the fewest lanes that still
+        // tile the output width (1920 -> 4 waves x 60 lanes x 8 outputs, no overlap)
+        const int lanes = (l.dstW + 7) / 8;
+        np = l.np > 0 ? min(l.np, 62) : (lanes + wpr - 1) / wpr;
+        if (np * 8 > l.dstW)
+            np = l.dstW / 8;
+        opw = 8 * np;
+        wpr = (l.dstW + opw - 1) / opw;
+    }
+    LanczosArgs a{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np};
     // buffer ranges: the source window spans rows [srcRow0, srcH) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(l.srcH - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -658,6 +855,27 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     const int waves = bands * wpr;
     dim3 grid(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
     const int pd = l.prefetch;
+    if (l.sym) {
+        const bool one = (l.cy[0] & 0xffffu) == 1u;
+        if (l.NY == 10 && one) {
+            if (pd <= 1)
+                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 1, true>), grid, dim3(256), 0, s, a);
+            else if (pd == 2)
+                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 2, true>), grid, dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 3, true>), grid, dim3(256), 0, s, a);
+        } else if (l.NY == 10) {
+            hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 2, false>), grid, dim3(256), 0, s, a);
+        } else {
+            if (pd <= 1)
+                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 1, false>), grid, dim3(256), 0, s, a);
+            else if (pd == 2)
+                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 2, false>), grid, dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 3, false>), grid, dim3(256), 0, s, a);
+        }
+        return hipGetLastError();
+    }
     if (l.NY == 10) {
         if (pd <= 1)
             hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 1>), grid, dim3(256), 0, s, a);

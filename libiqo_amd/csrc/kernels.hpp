@@ -44,6 +44,11 @@ struct LanczosDev {
     int yTopS[16], yBotS[16], xT[8];
     int dbg;                     // timing experiments only (see kernels.hip)
     int prefetch;                // prefetch depth in output rows (1..3)
+    // symmetric streamer (plan.hpp FastLanczos::sym)
+    int sym;                     // 1: lanczos_sym_kernel, 0: accumulator-ring streamer
+    int NX, offXO;               // unpadded X taps, odd first tap column
+    uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table
+    int np;                      // producing lanes per wave (0 = auto)
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,

@@ -508,6 +508,14 @@ void pick_fast_lanczos(Plan *p)
     // (2,2,8,10,-2) Lanczos-2 2:1.  Everything else runs the general kernel.
     bool inst = KY == 2 && KX == 2 && ((f.NY == 10 && f.NXP == 14 && f.offX == -6) ||
                                        (f.NY == 8 && f.NXP == 10 && f.offX == -4));
+    // symmetric variant: (NY, NX, offXO) = (10, 12, -5) Lanczos-3 2:1, (8, 8, -3) Lanczos-2 2:1
+    f.NX = xh - xl;
+    f.offXO = off;
+    f.cxo.assign(x.table.begin() + xl, x.table.begin() + xh);
+    bool symY = (f.NY % 2) == 0;
+    for (int i = 0; symY && i < f.NY / 2; ++i)
+        symY = f.cy[static_cast<size_t>(i)] == f.cy[static_cast<size_t>(f.NY - 1 - i)];
+    f.sym = inst && symY && (off & 1) && ((f.NY == 10 && f.NX == 12 && off == -5) || (f.NY == 8 && f.NX == 8 && off == -3));
     if (!inst || (p->srcW % 16) || p->srcW > 8192)
         return;
     p->kernel = 1;  // IQO_KERNEL_LANCZOS_STREAM

@@ -55,6 +55,13 @@ struct FastLanczos {
     int offX = 0;                 // first (padded) tap column = KX*x + offX (even)
     std::vector<int16_t> cy;      // NY
     std::vector<int16_t> cx;      // NXP (zero padded)
+    // Symmetric streamer (kernels.hip lanczos_sym_kernel): symmetric Y table of even length,
+    // X taps unpadded with an odd first column, so the taps of every output fall on odd-aligned
+    // column pairs.
+    bool sym = false;
+    int NX = 0;                   // X taps after trimming zero coefficients (even)
+    int offXO = 0;                // first tap column = KX*x + offXO (odd)
+    std::vector<int16_t> cxo;     // NX
     int mainBeginY = 0, mainEndY = 0, mainBeginX = 0, mainEndX = 0;
     std::vector<int32_t> denoYTop, denoYBot; // wrapped int16 valid-tap sums per border row
     std::vector<int32_t> dXLeft, dXRight;    // 64 * valid-tap sum per border column

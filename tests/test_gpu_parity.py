@@ -155,6 +155,39 @@ def test_row_band_sharding_is_byte_identical(cfg):
     assert torch.equal(torch.cat(parts, dim=1), full)
 
 
+STREAM_SHAPES = [
+    (3, 3840, 2160, 1920, 1080),  # C2: 4 waves x 60 lanes per row
+    (2, 3840, 2160, 1920, 1080),
+    (2, 640, 480, 320, 240),      # C1 shape: one wave of 40 lanes per row
+    (3, 1936, 1090, 968, 545),    # odd output height, right-edge wave overlaps its neighbour
+    (3, 4000, 64, 2000, 32),      # short bands, 5 waves per row
+    (2, 2064, 40, 1032, 20),
+]
+
+
+@pytest.mark.parametrize("shape", STREAM_SHAPES, ids=lambda s: "L%d_%dx%d" % s[:3])
+def test_stream_variants_agree_with_oracle(shape):
+    """Both Lanczos streamers (symmetric window and accumulator ring), every prefetch depth, forced
+    lane counts and band splits produce the oracle's output."""
+    d, sw, sh, dw, dh = shape
+    frames = _noise_batch(2, sw, sh, 300)
+    frames[1, :, : sw // 5] = 255
+    src = torch.from_numpy(frames).to(DEV)
+    exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 1, frames[f]) for f in range(2)]
+    for variant, pd, lanes, bands in [(0, 1, 0, 0), (0, 2, 0, 7), (0, 3, 0, 0), (0, 2, 62, 3), (0, 3, 33, 0),
+                                      (1, 3, 0, 0), (1, 1, 0, 5)]:
+        r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
+        assert r.describe()["kernel"] == "lanczos_stream"
+        r.set_option("stream_variant", variant)
+        r.set_option("prefetch", pd)
+        r.set_option("lanes", lanes)
+        r.set_option("bands", bands)
+        out = r.resize_tensor(src).cpu().numpy()
+        for f in range(2):
+            bad = np.argwhere(out[f] != exp[f])
+            assert bad.size == 0, (shape, variant, pd, lanes, bands, f, bad[:4].tolist())
+
+
 @pytest.mark.parametrize("value", [0, 255])
 def test_flat_frames_stay_flat_full_size(value):
     for m, d, sw, sh, dw, dh, px in CONFIGS[:3]:
