@@ -133,6 +133,8 @@ def main():
     ap.add_argument("--force-general", action="store_true")
     ap.add_argument("--debug-flags", type=int, default=0, help="timing experiments (wrong output)")
     ap.add_argument("--prefetch", type=int, default=0, help="Lanczos streamer prefetch depth (0 = default)")
+    ap.add_argument("--variant", type=int, default=-1, help="Lanczos streamer: 0 symmetric, 1 ring (A/B)")
+    ap.add_argument("--lanes", type=int, default=0, help="symmetric streamer producing lanes per wave (0 = auto)")
     args = ap.parse_args()
 
     import torch
@@ -164,6 +166,10 @@ def main():
         r.set_option("debug_flags", args.debug_flags)
     if args.prefetch and kernel_is_lanczos(m, r):
         r.set_option("prefetch", args.prefetch)
+    if args.variant >= 0 and kernel_is_lanczos(m, r):
+        r.set_option("stream_variant", args.variant)
+    if args.lanes and kernel_is_lanczos(m, r):
+        r.set_option("lanes", args.lanes)
     kernel = r.describe()["kernel"]
 
     gen = torch.Generator(device=dev)

@@ -32,7 +32,7 @@ struct iqo_hip_plan {
     bool forceGeneral = false;
     int bands = 0;
     int debugFlags = 0;
-    int prefetch = 3;  // best of the 1/2/3 sweep on C2 (straight-line streamer)
+    int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
     int streamVariant = 0;  // 0: symmetric streamer where eligible, 1: accumulator-ring streamer
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     hipStream_t stream = nullptr;
@@ -405,7 +405,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "prefetch")) {  // Lanczos streamer prefetch depth (rows)
-        if (value < 1 || value > 3)
+        if (value < 1 || value > 4)
             return IQO_HIP_EINVAL;
         h->prefetch = static_cast<int>(value);
         return IQO_HIP_OK;

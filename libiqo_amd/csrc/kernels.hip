@@ -263,7 +263,8 @@ struct LanczosArgs {
     int srcBytes, dstBytes;  // extent of one frame's source window / destination band (buffer range)
     int bands, wavesPerRow;  // wave grid per frame: band-major, column-minor
     int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
-                             // 2 = no source loads.  0 in production.
+                             // 2 = no source loads, 4 = no edge columns, 8 = no border rows
+                             // (wrong output).  0 in production.
     int np;                  // producing lanes per wave (symmetric streamer)
 };
 
@@ -459,9 +460,10 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 
 // ================================================================ symmetric Lanczos streamer
 //
-// Same wave geometry and border handling as the ring streamer above, but the arithmetic is laid
-// out for gfx950's issue rates (scripts/ubench/isa_rate*.hip on MI355X): VOP2 adds and logic ops
-// issue in 2 cycles per wave, while v_pk_mad_u16, v_dot2*, v_perm and DPP moves take 4.
+// Same wave geometry and border semantics as the ring streamer above, but the arithmetic and the
+// memory pipeline are laid out for gfx950's issue rates (scripts/ubench/isa_rate*.hip on MI355X):
+// VOP2 adds and logic ops issue in 2 cycles per wave, while v_pk_mad_u16, v_dot2*, v_perm and DPP
+// moves take 4, so the kernel is VALU-bound unless the packed MACs are halved.
 //
 //  * Vertical: the 2:1 Lanczos Y table is symmetric (c_i == c_{NY-1-i}), so the work value is
 //    sum_{p < NY/2} c_p * (s[top+p] + s[top+NY-1-p]).  The pair sums of unpacked u16 bytes are
@@ -473,23 +475,61 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 //  * Horizontal: bytes are unpacked into ODD-aligned pairs Q_j = (cb+2j-1, cb+2j) (the lane's
 //    own pairs j = 1..8; byte cb+16 comes from the right neighbour by DPP).  The taps of output
 //    x start at the odd column 2x + offXO, so each output is exactly NX/2 v_dot2_i32_i16 on
-//    Q_{k+p+JLO} with no zero padding.
-//  * The first dot of every output takes the rounding bias from a VGPR (VOP3P form), and the
-//    DPP neighbour moves use bound_ctrl, so neither needs an initialising move.
+//    Q_{k+p+JLO} with no zero padding.  The first dot takes the rounding bias from a VGPR (VOP3P
+//    form) and DPP moves use bound_ctrl, so neither needs an initialising move.
+//  * Memory: each wave streams its rows through a private LDS ring of K slots (2 rows of 1 KiB
+//    each) filled by LDS-DMA (buffer_load_dwordx4 ... lds), K-1 output rows ahead of use.  The
+//    prefetch costs no VGPRs, so it can be deeper than a register ring, and the slot index is a
+//    runtime value, so the unroll is only NY/2 (the window period).  The DMA is issued from
+//    inline asm with explicit vmcnt accounting (the compiler would drain vmcnt(0) before every
+//    LDS read of a DMA target): in program order every iteration issues 2 DMAs and 1 store, the
+//    prologue issues K-1 dropped stores so that the pattern holds from the first iteration, and
+//    iteration i waits with vmcnt(3K-5), which retires exactly DMA(i).
+//  * Edge waves (holding the <= 4 border columns per side) run their own copy of the loop, so
+//    the border-column divisions cost nothing in the other waves.
 //  * A wave has np producing lanes (1..np) and halo lanes 0 and np+1; the host sizes np so the
 //    waves of a row tile the output width exactly when it can (1920 = 4 x 60 x 8).  Idle lanes
-//    (> np+1) load nothing (out-of-range offsets) and store nothing.
-//  * Rows past the band's last needed source row are loaded out of range (no HBM traffic).
+//    (> np+1) load nothing (out-of-range offsets) and store nothing.  Rows past the band's last
+//    needed source row are loaded out of range too (no HBM traffic).
 
-template <int NY, int NX, int OFFX, int PD, bool C0ONE>
-__global__ __launch_bounds__(256, 3) void lanczos_sym_kernel(LanczosArgs a)
+// 16-byte-per-lane LDS-DMA of one source row into LDS bytes [lds, lds + 1024) of this wave.
+// M0 is saved and restored inside the statement (it is compiler-reserved).
+__device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff, bool nt = true)
+{
+    uint32_t keep;
+    if (nt)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
+                     : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
+                     : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt field");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NY, int NX, int OFFX, int K, bool C0ONE>
+__global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 {
     constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
     static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
-    constexpr int LV = H * PD / cgcd(H, PD);    // unroll: window slot x prefetch slot
+    static_assert(K >= 2 && 3 * K - 5 >= 0, "ring depth");
     constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
     constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
     static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
+    constexpr int SLOT = 2048;                  // bytes per ring slot (2 rows x 64 lanes x 16 B)
+    __shared__ __attribute__((aligned(16))) uint8_t ring[4 * K * SLOT];
+    __shared__ int4 edgeSum[4][2][64];          // per wave: parked border-column sums, 64 rows
 
     const LanczosDev &L = a.l;
     const int lane = static_cast<int>(threadIdx.x) & 63;
@@ -509,7 +549,7 @@ __global__ __launch_bounds__(256, 3) void lanczos_sym_kernel(LanczosArgs a)
     const int outX = x0 + (lane - 1) * 8;
     const bool produce = lane >= 1 && lane <= np && outX < L.dstW;
     const int voff = (lane <= np + 1 && cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;
-    const bool edgeL = x0 == 0, edgeR = x0 + opw >= L.dstW;
+    const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
     const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
@@ -522,20 +562,34 @@ __global__ __launch_bounds__(256, 3) void lanczos_sym_kernel(LanczosArgs a)
     const int dbg = a.dbg;
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
     const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
-    // last source row the band reads: rows beyond it (prefetch overrun) are loaded out of range
-    const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;
-    const uint32_t bias = opaque(1u << 19);  // rounding bias in a VGPR (VOP3P src2 of the first dot)
+    const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;  // last source row the band reads
+    const uint32_t bias = opaque(1u << 19);            // rounding bias (VOP3P src2 of the first dot)
 
-    auto load_row = [&](int r) -> uint4 {
-        const int so = r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000;
-        u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, so, 2 /* nt */);
-        return make_uint4(q.x, q.y, q.z, q.w);
+    // LDS ring of this wave: iteration i's two rows live in slot i mod K
+    const uint32_t ldsWave = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+                                 (__attribute__((address_space(3))) uint8_t *)ring)) +
+                             static_cast<uint32_t>(wib * K * SLOT);
+    const uint8_t *ringLane = ring + wib * K * SLOT + lane * 16;
+    auto row_soff = [&](int r) { return r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000; };
+    // iteration i (output row y0 + i) brings source rows rowBase + 2i + NY - 2, + NY - 1
+    const int rowBase = 2 * y0 + L.offY;
+    auto dma_iter = [&](int i) {
+        const uint32_t s = ldsWave + static_cast<uint32_t>((i % K) * SLOT);
+        const int r = rowBase + 2 * i + NY - 2;
+        dma_row(s, svoff, srcR, row_soff(r));
+        dma_row(s + 1024, svoff, srcR, row_soff(r + 1));
     };
-    // odd-aligned u16 pairs Q_1..Q_8 of one row: (b1,b2) (b3,b4) ... (b15, b16), b16 = right
+    auto read_iter = [&](int i, uint4 &r0, uint4 &r1) {
+        const uint8_t *p = ringLane + (i % K) * SLOT;
+        r0 = *reinterpret_cast<const uint4 *>(p);
+        r1 = *reinterpret_cast<const uint4 *>(p + 1024);
+    };
+
+    // odd-aligned u16 pairs Q_1..Q_8 of one row: (b1,b2) (b3,b4) ... (b15,b16), b16 = right
     // neighbour's byte 0
     auto unpack_odd = [&](uint4 v, uint32_t (&q)[8]) {
-        const uint32_t r = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v.x), 0x130 /* wave_shl:1 */,
-                                                                          0xf, 0xf, true));
+        const uint32_t r = static_cast<uint32_t>(
+            __builtin_amdgcn_mov_dpp(static_cast<int>(v.x), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
         q[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c020c01u);
         q[1] = __builtin_amdgcn_perm(v.y, v.x, 0x0c040c03u);
         q[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c020c01u);
@@ -546,100 +600,137 @@ __global__ __launch_bounds__(256, 3) void lanczos_sym_kernel(LanczosArgs a)
         q[7] = __builtin_amdgcn_perm(r, v.w, 0x0c040c03u);
     };
 
-    // window: at output row i the NY source rows rowBase + 2(i - y0) + t (t < NY) live in
-    // slots (2(i - y0) + t) mod NY; iteration i brings the last two (t = NY-2, NY-1)
+    // Border columns of rows [yb, yb + n) from the parked sums: floor(max(S, 0) / D) with the
+    // exact multiply-high constants of plan.cpp magic_x (identity for the interior columns of the
+    // edge lane), clamped to a byte, one dword per row and side -- stored after the row's main
+    // store, so it overwrites those 4 bytes.
+    auto flush_edges = [&](int yb, int n) {
+        auto fix = [&](int sv, int k) {
+            const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.xM[k]) >> L.xT[k];
+            return min(qq, 255u);
+        };
+        const int rowOff = (yb + lane - a.io.dstRow0) * dstSt;
+        if (edgeL) {
+            const int4 e = edgeSum[wib][0][lane & 63];
+            const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff : 0x7ff00000, 0, 0);
+        }
+        if (edgeR) {
+            const int4 e = edgeSum[wib][1][lane & 63];
+            const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff + L.dstW - 4 : 0x7ff00000,
+                                                  0, 0);
+        }
+    };
+
+    // window: at output row y0 + i the NY source rows rowBase + 2i + t (t < NY) live in slots
+    // (2i + t) mod NY; iteration i brings the last two (t = NY-2, NY-1)
     uint32_t win[NY][8];
-    const int iStart = y0;
-    const int rowBase = 2 * y0 + L.offY;  // first source row of output row y0
-    uint4 pre[PD][2];
+    {
+        // rows rowBase .. rowBase + NY - 3 go straight to VGPRs (window slots 0 .. NY-3)
+        uint4 w0[NY - 2];
 #pragma unroll
-    for (int i = 0; i < PD; ++i)
+        for (int t = 0; t < NY - 2; ++t) {
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowBase + t), 2 /* nt */);
+            w0[t] = make_uint4(q.x, q.y, q.z, q.w);
+        }
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-            pre[i][j] = load_row(rowBase + 2 * i + NY - 2 + j);
-    // rows rowBase .. rowBase + NY - 3 (window slots 0 .. NY-3) before the first iteration
+        for (int t = 0; t < NY - 2; ++t)
+            unpack_odd(w0[t], win[t]);
+    }
+    // ring prologue: DMA(0) .. DMA(K-2), each followed by a dropped store, so that from the first
+    // iteration on the vm counter sees the steady-state order DMA(j), S(j-K+1)
 #pragma unroll
-    for (int t = 0; t < NY - 2; ++t)
-        unpack_odd(load_row(rowBase + t), win[t]);
+    for (int j = 0; j < K - 1; ++j) {
+        dma_iter(j);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, 0x7ff00000, 0, 0);
+    }
 
-    for (int base = iStart; base < y1; base += LV) {
-        static_for<LV>([&](auto uc) {
-            constexpr int v = decltype(uc)::value;
-            constexpr int ps = v % PD;
-            const int yy = base + v;
-            // the two new rows of this iteration -> window slots (2v + NY - 2) mod NY, +1
-            unpack_odd(pre[ps][0], win[(2 * v + NY - 2) % NY]);
-            unpack_odd(pre[ps][1], win[(2 * v + NY - 1) % NY]);
-            const int rNext = rowBase + 2 * (yy + PD - iStart) + NY - 2;
-            pre[ps][0] = load_row(rNext);
-            pre[ps][1] = load_row(rNext + 1);
-            if (yy >= y1)
-                return;  // past the band end (uniform)
+    auto row = [&](auto uc, int base) {
+        constexpr int v = decltype(uc)::value;
+        const int i = base + v;  // iteration = output row y0 + i
+        const int yy = y0 + i;
+        if (yy >= y1)
+            return;  // past the band end (uniform)
+        // DMA(i) retired: after it come 2 DMAs per later iteration (K-2 of them) and the
+        // K-1 stores of iterations i-K+1 .. i-1
+        wait_vmcnt<3 * K - 5>();
+        uint4 n0, n1;
+        read_iter(i, n0, n1);
+        dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
+        unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
+        unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
 
-            // vertical: pair p = slots (2v + p, 2v + NY - 1 - p) mod NY
-            uint32_t acc[8];
+        // vertical: pair p = slots (2v + p, 2v + NY - 1 - p) mod NY
+        uint32_t acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t p0 = win[(2 * v) % NY][c] + win[(2 * v + NY - 1) % NY][c];
+            acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
+        }
+#pragma unroll
+        for (int p = 1; p < H; ++p)
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const uint32_t p0 = win[(2 * v) % NY][c] + win[(2 * v + NY - 1) % NY][c];
-                acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
+                const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
+                acc[c] = pk_mad(pp, L.cy[p], acc[c]);
             }
+        if ((yy < L.mainBeginY || yy >= L.mainEndY) && !(dbg & 8)) {
+            // border row (uniform, rare): rows outside the image were read as zero
+            const bool top = yy < L.mainBeginY;
+            const int bi = top ? yy : yy - L.mainEndY;
+            const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
+            const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
 #pragma unroll
-            for (int p = 1; p < H; ++p)
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
-                    acc[c] = pk_mad(pp, L.cy[p], acc[c]);
-                }
-            if (yy < L.mainBeginY || yy >= L.mainEndY) {
-                // border row (uniform, rare): rows outside the image were read as zero
-                const bool top = yy < L.mainBeginY;
-                const int bi = top ? yy : yy - L.mainEndY;
-                const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
-                const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
-#pragma unroll
-                for (int c = 0; c < 8; ++c)
-                    acc[c] = ydiv2(acc[c], m, sh);
-            }
+            for (int c = 0; c < 8; ++c)
+                acc[c] = ydiv2(acc[c], m, sh);
+        }
 
-            // Q_j for j in [JLO, JHI): own pairs 1..8, neighbours' by DPP
-            uint32_t q[JHI - JLO];
+        // Q_j for j in [JLO, JHI): own pairs 1..8, neighbours' by DPP
+        uint32_t q[JHI - JLO];
 #pragma unroll
-            for (int j = JLO; j < JHI; ++j) {
-                if (j <= 0)
-                    q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
-                        static_cast<int>(acc[j + 7]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
-                else if (j >= 9)
-                    q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
-                        static_cast<int>(acc[j - 9]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
-                else
-                    q[j - JLO] = acc[j - 1];
+        for (int j = JLO; j < JHI; ++j) {
+            if (j <= 0)
+                q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
+                    static_cast<int>(acc[j + 7]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+            else if (j >= 9)
+                q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
+                    static_cast<int>(acc[j - 9]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+            else
+                q[j - JLO] = acc[j - 1];
+        }
+        int sum[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            int sacc;  // VOP3P form: the bias VGPR is src2, no copy into the accumulator
+            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[0]), "v"(q[k]), "v"(bias));
+#pragma unroll
+            for (int p = 1; p < NX / 2; ++p)
+                sacc = sdot2(q[k + p], L.cxo[p], sacc);
+            sum[k] = sacc;
+        }
+        u32x2 o;
+        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        if (edgeL || edgeR) {
+            // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
+            // LDS; every 64 rows and at the band end one pass divides them, one row per lane
+            const int slot = i & 63;
+            if (edgeL && laneL)
+                edgeSum[wib][0][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+            if (edgeR && laneR)
+                edgeSum[wib][1][slot] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+            if (slot == 63 || yy == y1 - 1) {
+                __builtin_amdgcn_wave_barrier();
+                flush_edges(yy - slot, slot + 1);  // after this row's main store (same addresses)
             }
-            int sum[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                int sacc = sdot2(q[k], L.cxo[0], static_cast<int>(bias));
-#pragma unroll
-                for (int p = 1; p < NX / 2; ++p)
-                    sacc = sdot2(q[k + p], L.cxo[p], sacc);
-                sum[k] = sacc;
-            }
-            if (edgeL || edgeR) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const bool side = k < 4 ? edgeL : edgeR;
-                    if (side) {
-                        const uint32_t n = static_cast<uint32_t>(max(sum[k], 0));
-                        const uint32_t qq = __umulhi(n, L.xM[k]) >> L.xT[k];
-                        sum[k] = (k < 4 ? laneL : laneR) ? static_cast<int>(qq << 20) : sum[k];
-                    }
-                }
-            }
-            u32x2 o;
-            o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
-            o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
-        });
-    }
+        }
+    };
+    for (int base = 0; y0 + base < y1; base += H)
+        static_for<H>([&](auto uc) { row(uc, base); });
+
+    wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
 
 // ================================================================ Area integer ratio
@@ -858,21 +949,17 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     if (l.sym) {
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         if (l.NY == 10 && one) {
-            if (pd <= 1)
-                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 1, true>), grid, dim3(256), 0, s, a);
-            else if (pd == 2)
-                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 2, true>), grid, dim3(256), 0, s, a);
-            else
+            if (pd <= 2)
                 hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 3, true>), grid, dim3(256), 0, s, a);
-        } else if (l.NY == 10) {
-            hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 2, false>), grid, dim3(256), 0, s, a);
-        } else {
-            if (pd <= 1)
-                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 1, false>), grid, dim3(256), 0, s, a);
-            else if (pd == 2)
-                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 2, false>), grid, dim3(256), 0, s, a);
             else
+                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 4, true>), grid, dim3(256), 0, s, a);
+        } else if (l.NY == 10) {
+            hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 4, false>), grid, dim3(256), 0, s, a);
+        } else {
+            if (pd <= 2)
                 hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 3, false>), grid, dim3(256), 0, s, a);
+            else
+                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 4, false>), grid, dim3(256), 0, s, a);
         }
         return hipGetLastError();
     }
