@@ -135,6 +135,8 @@ def main():
     ap.add_argument("--prefetch", type=int, default=0, help="Lanczos streamer prefetch depth (0 = default)")
     ap.add_argument("--variant", type=int, default=-1, help="Lanczos streamer: 0 symmetric, 1 ring (A/B)")
     ap.add_argument("--lanes", type=int, default=0, help="symmetric streamer producing lanes per wave (0 = auto)")
+    ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra plan option (iqo_hip_plan_set_option), repeatable")
     args = ap.parse_args()
 
     import torch
@@ -170,6 +172,9 @@ def main():
         r.set_option("stream_variant", args.variant)
     if args.lanes and kernel_is_lanczos(m, r):
         r.set_option("lanes", args.lanes)
+    for kv in args.option:
+        k, v = kv.split("=", 1)
+        r.set_option(k, int(v))
     kernel = r.describe()["kernel"]
 
     gen = torch.Generator(device=dev)

@@ -33,6 +33,7 @@ struct iqo_hip_plan {
     int bands = 0;
     int debugFlags = 0;
     int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
+    int linPrefetch = 0;    // Linear 2x streamer: source rows in flight per wave (0 = default 2)
     int streamVariant = 0;  // 0: symmetric streamer where eligible, 1: accumulator-ring streamer
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     hipStream_t stream = nullptr;
@@ -310,7 +311,10 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
                 l.cx[q] = pair16(p.fln.cx[q][0], p.fln.cx[q][1]);
                 l.cy[q] = pair16(p.fln.cy[q][0], p.fln.cy[q][1]);
             }
-            e = iqo_amd::launch_linear_up2(l, io, rb, re, s);
+            l.dbg = h->debugFlags;
+            l.prefetch = h->linPrefetch;
+            int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
+            e = iqo_amd::launch_linear_up2(l, io, rb, re, bands, s);
         } else {
             iqo_amd::GeneralDev g{};
             g.method = p.method;
@@ -408,6 +412,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 1 || value > 4)
             return IQO_HIP_EINVAL;
         h->prefetch = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "lin_prefetch")) {  // Linear 2x streamer: source rows in flight (2, 4, 8)
+        if (value != 0 && value != 2 && value != 4 && value != 8)
+            return IQO_HIP_EINVAL;
+        h->linPrefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric (default), 1 ring

@@ -792,101 +792,180 @@ __global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
     }
 }
 
-// ================================================================ exact 2x bilinear upsampler
+// ================================================================ exact 2x bilinear streamer
 //
-// Thread = 16 output columns of one output row; it needs work columns [8t-1, 8t+8] of the two
-// source rows (interior: o = (y-1)>>1, phase y&1).  Bytes are gathered straight into
-// odd-aligned u16 pairs P_q = (8t-1+2q, 8t+2q); even pairs come from v_alignbit.
+// One WAVE = one row band of one frame x one strip of source columns, walking the band top to
+// bottom so every source row is fetched from HBM once per band (2x upsampling reads each source
+// row for four output rows; a per-row kernel re-fetched it from L2/MALL each time).
+//
+// Lane l owns the 8 source columns [cb, cb + 8), cb = x0 - 8 + 8l, and (lanes 1..np) the 16
+// output columns [2cb, 2cb + 16), which read work columns [cb - 1, cb + 8]: the two outer ones
+// come from the neighbouring lanes by DPP before unpacking, so each source row is one 8-B
+// coalesced load + 2 DPP + 5 v_perm into odd-aligned u16 pairs P_q = (cb-1+2q, cb+2q).
+//
+// Output rows 2k+1 (phase 1) and 2k+2 (phase 0) both blend source rows k and k+1
+// (IQOLinearResizerImpl_Generic.cpp:308-325 with o = (y-1)/2 at exact 2x); rows 0 and dstH-1 are
+// the replicated first / last source row x 256 (:290-299).  Horizontally output 2cb+j blends
+// work columns m, m+1 with m = cb + floor((j-1)/2) and phase j&1 (:374-407): one v_dot2_u32_u16
+// per output; (S + 2^22) >> 23 <= 255 always (S <= 65280 * 2^15), so the reference's
+// int16 -> u16 clamp is a no-op and the bytes pack with v_ashr_pk_u8_i32.  Columns 0 and dstW-1
+// are replicated borders (:343-366): their lanes use a per-lane weight pair (no branch).
+//
+// The row loop is straight-line (unrolled by the prefetch depth PD, statically named registers)
+// and its memory stream branch-free: rows past the band's last source row and stores of rows
+// outside the band use out-of-range buffer offsets (no traffic, exact waitcnt accounting).
 
 struct LinearArgs {
     LinearDev g;
     Io io;
-    int rowBegin, rowEnd, groups;
+    int rowBegin, rowEnd, rowsPerBand;
+    int srcBytes, dstBytes;
+    int bands, wavesPerRow, np;
 };
 
-__device__ __forceinline__ void gather_pairs(const uint8_t *row, int t, int srcW, uint32_t (&P)[5])
+// v_ashr_pk_u8_i32 with shift 23: (sat_u8(a >> 23), sat_u8(b >> 23)) into the low / high half
+__device__ __forceinline__ uint32_t pack23_lo(uint32_t a, uint32_t b)
 {
-    // bytes [8t-4, 8t+12) as four dwords, clamped inside the row (clamped bytes feed only the
-    // replicated border columns, which do not read them)
-    int c0 = max(8 * t - 4, 0);
-    int c2 = min(8 * t + 8, srcW - 4);
-    uint32_t d0 = *reinterpret_cast<const uint32_t *>(row + c0);
-    uint2 d12 = *reinterpret_cast<const uint2 *>(row + 8 * t);
-    uint32_t d3 = *reinterpret_cast<const uint32_t *>(row + c2);
-    P[0] = __builtin_amdgcn_perm(d12.x, d0, 0x0c040c03u);
-    P[1] = __builtin_amdgcn_perm(0u, d12.x, 0x0c020c01u);
-    P[2] = __builtin_amdgcn_perm(d12.y, d12.x, 0x0c040c03u);
-    P[3] = __builtin_amdgcn_perm(0u, d12.y, 0x0c020c01u);
-    P[4] = __builtin_amdgcn_perm(d3, d12.y, 0x0c040c03u);
+    uint32_t w;
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 23" : "=v"(w) : "v"(a), "v"(b));
+    return w;
+}
+__device__ __forceinline__ uint32_t pack23_hi(uint32_t w, uint32_t a, uint32_t b)
+{
+    asm("v_ashr_pk_u8_i32 %0, %1, %2, 23 op_sel:[0,0,0,1]" : "+v"(w) : "v"(a), "v"(b));
+    return w;
 }
 
+template <int PD, bool NTST>
 __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 {
-    const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    const int64_t total = static_cast<int64_t>(a.rowEnd - a.rowBegin) * a.groups;
-    if (gid >= total)
-        return;
+    static_assert(PD % 2 == 0, "the unroll must also cover the 2-slot row ring");
     const LinearDev &g = a.g;
-    const int y = a.rowBegin + static_cast<int>(gid / a.groups);
-    const int t = static_cast<int>(gid % a.groups);
-    const uint8_t *srcF = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
-    auto row_ptr = [&](int r) { return srcF + static_cast<int64_t>(r - a.io.srcRow0) * a.io.srcSt; };
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const int gw = static_cast<int>(blockIdx.x) * 4 + wib;
+    if (gw >= a.bands * a.wavesPerRow)
+        return;
+    const int band = gw / a.wavesPerRow, wcol = gw - band * a.wavesPerRow;
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int np = a.np;
+    const int x0 = max(0, min(wcol * 8 * np, g.srcW - 8 * np));  // first source column of lane 1
+    const int cb = x0 - 8 + 8 * lane;
+    const bool produce = lane >= 1 && lane <= np;
+    const int voff = (lane <= np + 1 && cb >= 0 && cb < g.srcW) ? cb : 0x7ff00000;
+    const int stoff = produce ? 2 * cb : 0x7ff00000;
+    // replicated border columns (work + 128) >> 8 == (work * 2^15 + 2^22) >> 23: the border lanes
+    // take the weight pair (0, 2^15) / (2^15, 0) for their outer output, so no branch is needed
+    const uint32_t cxFirst = cb == 0 ? 0x80000000u : g.cx[0];
+    const uint32_t cxLast = cb + 8 == g.srcW ? 0x00008000u : g.cx[1];
 
-    uint32_t W[5];  // work pairs (u16) at odd alignment
-    if (y == 0 || y == g.dstH - 1) {
-        // replicated first / last source row: work = src * 256 (:290-299)
-        uint32_t P[5];
-        gather_pairs(row_ptr(y == 0 ? 0 : g.srcH - 1), t, g.srcW, P);
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-            W[q] = pk_mul(P[q], 0x01000100u);
-    } else {
-        const int o = (y - 1) >> 1;
-        const uint32_t c = g.cy[y & 1];
-        uint32_t P0[5], P1[5];
-        gather_pairs(row_ptr(o), t, g.srcW, P0);
-        gather_pairs(row_ptr(o + 1), t, g.srcW, P1);
-        const uint32_t c0 = (c & 0xffffu) * 0x10001u, c1 = (c >> 16) * 0x10001u;
-#pragma unroll
-        for (int q = 0; q < 5; ++q)
-            W[q] = pk_mad(P1[q], c1, pk_mul(P0[q], c0));
-    }
-    uint32_t E[4];  // even-aligned pairs (8t+2q, 8t+2q+1)
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        E[q] = __builtin_amdgcn_alignbit(W[q + 1], W[q], 16);
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
 
-    uint32_t outw[4];
+    // interior output rows of the band: [max(y0, 1), yl); pair index k covers rows 2k+1, 2k+2
+    const int yl = min(y1, g.dstH - 1);
+    const int kLo = y0 <= 1 ? 0 : (y0 - 1) >> 1;
+    const int kHi = yl >> 1;  // exclusive
+    const int rLast = kHi;    // last source row the loop reads
+
+    auto load_row = [&](int r) -> u32x2 {
+        return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff, r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000,
+                                                    2 /* nt */);
+    };
+    auto unpack = [&](u32x2 v, uint32_t (&P)[5]) {
+        const uint32_t left = static_cast<uint32_t>(
+            __builtin_amdgcn_mov_dpp(static_cast<int>(v.y), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+        const uint32_t right = static_cast<uint32_t>(
+            __builtin_amdgcn_mov_dpp(static_cast<int>(v.x), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        P[0] = __builtin_amdgcn_perm(v.x, left, 0x0c040c03u);   // (cb-1, cb)
+        P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c020c01u);     // (cb+1, cb+2)
+        P[2] = __builtin_amdgcn_perm(v.y, v.x, 0x0c040c03u);    // (cb+3, cb+4)
+        P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c020c01u);     // (cb+5, cb+6)
+        P[4] = __builtin_amdgcn_perm(right, v.y, 0x0c040c03u);  // (cb+7, cb+8)
+    };
+    // horizontal pass + store of one output row from its odd-aligned work pairs
+    auto emit = [&](const uint32_t (&W)[5], int y, bool valid) {
+        uint32_t E[4];  // even-aligned pairs (cb+2q, cb+2q+1)
 #pragma unroll
-    for (int j4 = 0; j4 < 4; ++j4) {
-        uint32_t word = 0;
+        for (int q = 0; q < 4; ++q)
+            E[q] = __builtin_amdgcn_alignbit(W[q + 1], W[q], 16);
+        uint32_t s[16];
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            const int j = 4 * j4 + jj;
-            const int r = (j - 1) >> 1;  // work column offset from 8t (floor)
-            const uint32_t pair = (r & 1) ? W[(r + 1) >> 1] : E[r >> 1];
-            uint32_t pairj = (j == 0) ? W[0] : pair;
-            uint32_t sum = udot2(pairj, g.cx[j & 1], 1u << 22);
-            uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(sum) >> 23));
-            uint32_t v = opaque(u > 255 ? 255u : u);
-            word |= v << (8 * jj);
+        for (int j = 0; j < 16; ++j) {
+            const int r = (j - 1) >> 1;
+            const uint32_t pr = j == 0 ? W[0] : ((r & 1) ? W[(r + 1) >> 1] : E[r >> 1]);
+            s[j] = udot2(pr, j == 0 ? cxFirst : (j == 15 ? cxLast : g.cx[j & 1]), 1u << 22);
         }
-        outw[j4] = word;
+        u32x4 o;
+        o.x = pack23_hi(pack23_lo(s[0], s[1]), s[2], s[3]);
+        o.y = pack23_hi(pack23_lo(s[4], s[5]), s[6], s[7]);
+        o.z = pack23_hi(pack23_lo(s[8], s[9]), s[10], s[11]);
+        o.w = pack23_hi(pack23_lo(s[12], s[13]), s[14], s[15]);
+        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, stoff, valid ? (y - dstRow0) * dstSt : 0x7ff00000,
+                                               NTST ? 2 : 0);
+    };
+    auto border_row = [&](int y, int r) {
+        uint32_t P[5];
+        unpack(__builtin_amdgcn_raw_buffer_load_b64(srcR, voff, (r - srcRow0) * srcSt, 2), P);
+#pragma unroll
+        for (int q = 0; q < 5; ++q)
+            P[q] = pk_mul(P[q], 0x01000100u);
+        emit(P, y, true);
+    };
+
+    if (y0 == 0)
+        border_row(0, 0);
+
+    const uint32_t c0a = (g.cy[1] & 0xffffu) * 0x10001u, c1a = (g.cy[1] >> 16) * 0x10001u;  // row 2k+1
+    const uint32_t c0b = (g.cy[0] & 0xffffu) * 0x10001u, c1b = (g.cy[0] >> 16) * 0x10001u;  // row 2k+2
+    uint32_t U[2][5];
+    u32x2 pre[PD];
+    unpack(load_row(kLo), U[0]);
+    // prologue in the loop's own vm-counter pattern (load, store, store per iteration; the
+    // stores are dropped) and issue order, so the waits at the loop header, which must hold for
+    // the preheader path too, are the steady-state ones and keep PD rows in flight
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        pre[i] = load_row(kLo + 1 + i);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, 0x7ff00000, 0x7ff00000 + 32 * i, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, 0x7ff00000, 0x7ff00010 + 32 * i, 0);
     }
-    // replicated border columns (:343-345, :360-365): x = 0 reads work[0], x = dstW-1 work[srcW-1]
-    if (t == 0) {
-        uint32_t w0 = W[0] >> 16;  // column 0 = high half of P_0 (columns -1, 0)
-        uint16_t u = static_cast<uint16_t>(static_cast<int16_t>((static_cast<int>(w0) + 128) >> 8));
-        outw[0] = (outw[0] & ~0xffu) | (u > 255 ? 255u : u);
+    for (int base = kLo; base < kHi; base += PD) {
+        static_for<PD>([&](auto uc) {
+            constexpr int v = decltype(uc)::value;
+            const int k = base + v;
+            // iterations past the band end (k >= kHi, fewer than PD) run on zero rows and drop
+            // their stores: no branch inside the loop keeps the vm-counter accounting exact
+            // keep iterations apart: otherwise the scheduler hoists all PD unpacks to the top
+            // of the trip and the wait for them drains the whole prefetch
+            __builtin_amdgcn_sched_barrier(0);
+            unpack(pre[v], U[(v + 1) % 2]);  // source row k + 1
+            pre[v] = load_row(k + 1 + PD);
+            const uint32_t(&A)[5] = U[v % 2];
+            const uint32_t(&B)[5] = U[(v + 1) % 2];
+            uint32_t W[5];
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                W[q] = pk_mad(B[q], c1a, pk_mul(A[q], c0a));
+            emit(W, 2 * k + 1, 2 * k + 1 >= y0 && 2 * k + 1 < yl);
+#pragma unroll
+            for (int q = 0; q < 5; ++q)
+                W[q] = pk_mad(B[q], c1b, pk_mul(A[q], c0b));
+            emit(W, 2 * k + 2, 2 * k + 2 >= y0 && 2 * k + 2 < yl);
+        });
     }
-    if (t == a.groups - 1) {
-        uint32_t wl = W[4] & 0xffffu;  // column 8t+7 = srcW-1 = low half of P_4
-        uint16_t u = static_cast<uint16_t>(static_cast<int16_t>((static_cast<int>(wl) + 128) >> 8));
-        outw[3] = (outw[3] & 0x00ffffffu) | ((u > 255 ? 255u : static_cast<uint32_t>(u)) << 24);
-    }
-    uint8_t *d = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt +
-                 static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt + 16 * t;
-    *reinterpret_cast<uint4 *>(d) = make_uint4(outw[0], outw[1], outw[2], outw[3]);
+
+    if (y1 == g.dstH && g.dstH > 1)
+        border_row(g.dstH - 1, g.srcH - 1);
 }
 
 } // namespace
@@ -1001,14 +1080,42 @@ hipError_t launch_area_int(const AreaDev &g, const Io &io, int rowBegin, int row
     return hipGetLastError();
 }
 
-hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
+hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, int bands,
+                             hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    LinearArgs a{g, io, rowBegin, rowEnd, g.dstW / 16};
-    int64_t total = static_cast<int64_t>(rowEnd - rowBegin) * a.groups;
-    dim3 grid(static_cast<unsigned>((total + 255) / 256), static_cast<unsigned>(io.frames));
-    hipLaunchKernelGGL(linear_up2_kernel, grid, dim3(256), 0, s, a);
+    if (g.srcW % 8 || g.dstW != 2 * g.srcW || g.srcW < 8)
+        return hipErrorInvalidValue;
+    const int rows = rowEnd - rowBegin;
+    bands = max(1, min(bands, rows));
+    const int rpb = (rows + bands - 1) / bands;
+    bands = (rows + rpb - 1) / rpb;
+    // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
+    const int lanes = g.srcW / 8;
+    int wpr = (lanes + 61) / 62;
+    int np = (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
+    LinearArgs a{g, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, np};
+    const int64_t sb = static_cast<int64_t>(g.srcH - io.srcRow0 - 1) * io.srcSt + g.srcW;
+    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + g.dstW;
+    if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31))
+        return hipErrorInvalidValue;
+    a.srcBytes = static_cast<int>(sb);
+    a.dstBytes = static_cast<int>(db);
+    const int waves = bands * wpr;
+    dim3 grid(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    // nontemporal stores by default (dbg 16 = plain stores, for A/B); 2 rows in flight per wave
+    // measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
+    const bool nt = !(g.dbg & 16);
+    const int pd = g.prefetch == 0 ? 2 : g.prefetch;
+    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a); };
+    if (pd >= 8)
+        nt ? go(linear_up2_kernel<8, true>) : go(linear_up2_kernel<8, false>);
+    else if (pd >= 4)
+        nt ? go(linear_up2_kernel<4, true>) : go(linear_up2_kernel<4, false>);
+    else
+        nt ? go(linear_up2_kernel<2, true>) : go(linear_up2_kernel<2, false>);
     return hipGetLastError();
 }
 

@@ -68,7 +68,10 @@ struct LinearDev {
     int srcW, srcH, dstW, dstH;
     uint32_t cy[2];              // per phase (c0, c1) u16 pairs
     uint32_t cx[2];
+    int dbg;                     // timing experiments: 16 = plain (not nontemporal) stores
+    int prefetch;                // source rows in flight per wave (2, 4, 8; 0 = default 2)
 };
-hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
+hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
+                             hipStream_t s);
 
 } // namespace iqo_amd

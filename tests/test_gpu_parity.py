@@ -188,6 +188,37 @@ def test_stream_variants_agree_with_oracle(shape):
             assert bad.size == 0, (shape, variant, pd, lanes, bands, f, bad[:4].tolist())
 
 
+LINEAR_UP2_SHAPES = [
+    (1920, 1080),  # C4: 4 waves x 60 lanes per row
+    (640, 480),    # 80 lanes: 2 waves x 40
+    (8, 1),        # one producing lane; both output rows are replicated borders
+    (24, 2),       # three lanes, one interior row pair
+    (504, 7),      # 63 lanes: 2 waves, the right-edge wave overlaps its neighbour
+    (1000, 33),
+]
+
+
+@pytest.mark.parametrize("shape", LINEAR_UP2_SHAPES, ids=lambda s: "%dx%d" % s)
+def test_linear_up2_streamer_variants(shape):
+    """The exact-2x Linear streamer at every prefetch depth and band split (bands starting on odd
+    and even rows, one-row bands, bands holding only a border row) produces the oracle's output."""
+    sw, sh = shape
+    dw, dh = 2 * sw, 2 * sh
+    frames = _noise_batch(2, sw, sh, 500)
+    frames[1, :, : max(1, sw // 5)] = 255
+    src = torch.from_numpy(frames).to(DEV)
+    exp = [ol.run_oracle("linear", 0, sw, sh, dw, dh, 1, frames[f]) for f in range(2)]
+    for pd, bands in [(0, 0), (2, 1), (4, 3), (8, 0), (2, dh), (4, max(1, dh // 2 + 1))]:
+        r = libiqo_amd.make_resizer("linear", 0, sw, sh, dw, dh, 1)
+        assert r.describe()["kernel"] == "linear_up2"
+        r.set_option("lin_prefetch", pd)
+        r.set_option("bands", bands)
+        out = r.resize_tensor(src).cpu().numpy()
+        for f in range(2):
+            bad = np.argwhere(out[f] != exp[f])
+            assert bad.size == 0, (shape, pd, bands, f, bad[:4].tolist())
+
+
 @pytest.mark.parametrize("value", [0, 255])
 def test_flat_frames_stay_flat_full_size(value):
     for m, d, sw, sh, dw, dh, px in CONFIGS[:3]:
