@@ -122,8 +122,8 @@ def read_pmc(config):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (0 = config default)")
     ap.add_argument("--bands", type=int, default=0, help="row bands per frame (0 = auto)")

@@ -34,8 +34,10 @@ struct iqo_hip_plan {
     int debugFlags = 0;
     int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
     int linPrefetch = 0;    // Linear 2x streamer: source rows in flight per wave (0 = default 2)
-    int streamVariant = 0;  // 0: symmetric streamer where eligible, 1: accumulator-ring streamer
+    int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
+                            // streamer, 2: per-wave symmetric streamer
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
+    int chunkFrames = 0;    // frames per launch (0 = auto: about kChunkBytes of frames)
     hipStream_t stream = nullptr;
     uint8_t *stageSrc = nullptr, *stageDst = nullptr;
     size_t stageSrcCap = 0, stageDstCap = 0;
@@ -45,6 +47,7 @@ namespace {
 
 constexpr int kChunkOut = 256;     // outputs per general-kernel chunk (= workgroup size)
 constexpr int kChunkLds = 8192;    // max work-row ints per chunk (32 KiB LDS)
+constexpr size_t kChunkBytes = size_t(1400) << 20;  // frames per launch of the fast kernels
 
 class DeviceGuard {  // restore the caller's current device
 public:
@@ -205,15 +208,6 @@ bool aligned(const void *p, size_t a, size_t st, size_t fst)
     return (reinterpret_cast<uintptr_t>(p) % a) == 0 && (st % a) == 0 && (fst % a) == 0;
 }
 
-int auto_bands(int rows, int frames)
-{
-    // Enough row bands to keep ~8 workgroups resident per CU on 256 CUs across the batch,
-    // while keeping bands tall (the 2-row halo per band is re-read).
-    const int target = 2048;
-    int bands = std::max(1, (target + frames - 1) / frames);
-    return std::max(1, std::min(bands, rows / 32 > 0 ? rows / 32 : 1));
-}
-
 int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t srcRow0, size_t srcSt,
              size_t srcFrameSt, const uint8_t *src, size_t dstSt, size_t dstFrameSt, uint8_t *dst, hipStream_t s)
 {
@@ -237,9 +231,22 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
         kernel = IQO_KERNEL_GENERAL;
 
     const int rb = static_cast<int>(r0), re = static_cast<int>(r0 + rows);
-    for (size_t f0 = 0; f0 < nFrames; f0 += 65535) {
+    // Frames per launch: at most 65535 (grid y), and for the fast kernels at most ~chunkBytes of
+    // frames (source window + output band): past ~1.3 GB per launch the same kernels lose
+    // 20-25 % of their HBM rate on MI355X (C2 at 160..256 frames per launch), while a launch
+    // boundary costs ~2 us.
+    size_t chunk = 65535;
+    if (kernel != IQO_KERNEL_GENERAL) {
+        const size_t perFrame = (p.srcH - srcRow0) * srcSt + rows * dstSt;
+        const size_t cap = h->chunkFrames > 0 ? static_cast<size_t>(h->chunkFrames)
+                                              : std::max<size_t>(1, kChunkBytes / std::max<size_t>(perFrame, 1));
+        chunk = std::min(chunk, cap);
+        const size_t n = (nFrames + chunk - 1) / chunk;  // equal launches, not one straggler
+        chunk = (nFrames + n - 1) / n;
+    }
+    for (size_t f0 = 0; f0 < nFrames; f0 += chunk) {
         iqo_amd::Io io;
-        io.frames = static_cast<int>(std::min<size_t>(65535, nFrames - f0));
+        io.frames = static_cast<int>(std::min(chunk, nFrames - f0));
         io.src = src + f0 * srcFrameSt;
         io.srcSt = static_cast<int64_t>(srcSt);
         io.srcFrameSt = static_cast<int64_t>(srcFrameSt);
@@ -282,14 +289,13 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             }
             l.dbg = h->debugFlags;
             l.prefetch = h->prefetch;
-            l.sym = f.sym && h->streamVariant != 1 ? 1 : 0;
+            l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant == 2 ? 2 : 1);
             l.NX = f.NX;
             l.offXO = f.offXO;
             for (int i = 0; i < f.NX / 2 && i < 8; ++i)
                 l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
             l.np = h->lanes;
-            int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
-            e = iqo_amd::launch_lanczos_stream(l, io, rb, re, bands, s);
+            e = iqo_amd::launch_lanczos_stream(l, io, rb, re, h->bands, s);
         } else if (kernel == IQO_KERNEL_AREA_INT) {
             iqo_amd::AreaDev a{};
             a.KY = p.far.KY;
@@ -313,8 +319,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             }
             l.dbg = h->debugFlags;
             l.prefetch = h->linPrefetch;
-            int bands = h->bands > 0 ? h->bands : auto_bands(re - rb, io.frames);
-            e = iqo_amd::launch_linear_up2(l, io, rb, re, bands, s);
+            e = iqo_amd::launch_linear_up2(l, io, rb, re, h->bands, s);
         } else {
             iqo_amd::GeneralDev g{};
             g.method = p.method;
@@ -420,8 +425,8 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->linPrefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric (default), 1 ring
-        if (value < 0 || value > 1)
+    if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric block-shared (default), 1 ring,
+        if (value < 0 || value > 2)              // 2 symmetric per-wave
             return IQO_HIP_EINVAL;
         h->streamVariant = static_cast<int>(value);
         return IQO_HIP_OK;
@@ -430,6 +435,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 62)
             return IQO_HIP_EINVAL;
         h->lanes = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "chunk_frames")) {  // frames per launch (0 = auto)
+        if (value < 0)
+            return IQO_HIP_EINVAL;
+        h->chunkFrames = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "bands")) {

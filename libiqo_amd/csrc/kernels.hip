@@ -11,6 +11,11 @@
 // v_dot2 (int16 / u16 pairs, int32 accumulate) for the horizontal taps.
 #include "kernels.hpp"
 
+#include <algorithm>
+#include <climits>
+#include <cstdint>
+#include <mutex>
+#include <unordered_map>
 #include <utility>
 
 namespace iqo_amd {
@@ -264,8 +269,9 @@ struct LanczosArgs {
     int bands, wavesPerRow;  // wave grid per frame: band-major, column-minor
     int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
                              // 2 = no source loads, 4 = no edge columns, 8 = no border rows
-                             // (wrong output).  0 in production.
+                             // (wrong output), 32 = all bands walk top-down.  0 in production.
     int np;                  // producing lanes per wave (symmetric streamer)
+    int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -518,6 +524,11 @@ __device__ __forceinline__ void wait_vmcnt()
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// cache policy of the symmetric streamer's output stores (experiments: 2 = nontemporal)
+#ifndef IQO_SYM_STORE_AUX
+#define IQO_SYM_STORE_AUX 0
+#endif
+
 template <int NY, int NX, int OFFX, int K, bool C0ONE>
 __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 {
@@ -562,7 +573,14 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
     const int dbg = a.dbg;
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
     const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
+    // Odd bands walk bottom-up: a band boundary's halo rows are then read by both bands at the
+    // same time (both at their start or both at their end) and the second read hits the
+    // Infinity Cache instead of HBM.  The window arithmetic is symmetric, so only the row order
+    // changes: walk index t of iteration i is source row rowAt(i, t).
+    const int dir = ((band & 1) && !(dbg & 32)) ? -1 : 1;
+    const int rFirst = 2 * y0 + L.offY;                 // first source row the band reads
     const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;  // last source row the band reads
+    const int nRows = y1 - y0;
     const uint32_t bias = opaque(1u << 19);            // rounding bias (VOP3P src2 of the first dot)
 
     // LDS ring of this wave: iteration i's two rows live in slot i mod K
@@ -570,14 +588,14 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
                                  (__attribute__((address_space(3))) uint8_t *)ring)) +
                              static_cast<uint32_t>(wib * K * SLOT);
     const uint8_t *ringLane = ring + wib * K * SLOT + lane * 16;
-    auto row_soff = [&](int r) { return r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000; };
-    // iteration i (output row y0 + i) brings source rows rowBase + 2i + NY - 2, + NY - 1
-    const int rowBase = 2 * y0 + L.offY;
+    auto row_soff = [&](int r) { return (r >= rFirst && r <= rLast) ? (r - srcRow0) * srcSt : 0x7ff00000; };
+    // iteration i (output row y0 + i, or y1 - 1 - i walking up) brings walk rows NY-2 and NY-1
+    auto rowAt = [&](int i, int t) { return dir > 0 ? rFirst + 2 * i + t : rLast - 2 * i - t; };
     auto dma_iter = [&](int i) {
         const uint32_t s = ldsWave + static_cast<uint32_t>((i % K) * SLOT);
-        const int r = rowBase + 2 * i + NY - 2;
+        const int r = rowAt(i, NY - 2);
         dma_row(s, svoff, srcR, row_soff(r));
-        dma_row(s + 1024, svoff, srcR, row_soff(r + 1));
+        dma_row(s + 1024, svoff, srcR, row_soff(r + dir));
     };
     auto read_iter = [&](int i, uint4 &r0, uint4 &r1) {
         const uint8_t *p = ringLane + (i % K) * SLOT;
@@ -609,7 +627,7 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
             const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.xM[k]) >> L.xT[k];
             return min(qq, 255u);
         };
-        const int rowOff = (yb + lane - a.io.dstRow0) * dstSt;
+        const int rowOff = (yb + dir * lane - a.io.dstRow0) * dstSt;
         if (edgeL) {
             const int4 e = edgeSum[wib][0][lane & 63];
             const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
@@ -623,15 +641,15 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
         }
     };
 
-    // window: at output row y0 + i the NY source rows rowBase + 2i + t (t < NY) live in slots
-    // (2i + t) mod NY; iteration i brings the last two (t = NY-2, NY-1)
+    // window: at iteration i the NY walk rows rowAt(i, t) (t < NY) live in slots (2i + t) mod NY;
+    // iteration i brings the last two (t = NY-2, NY-1)
     uint32_t win[NY][8];
     {
-        // rows rowBase .. rowBase + NY - 3 go straight to VGPRs (window slots 0 .. NY-3)
+        // walk rows 0 .. NY-3 of iteration 0 go straight to VGPRs (window slots 0 .. NY-3)
         uint4 w0[NY - 2];
 #pragma unroll
         for (int t = 0; t < NY - 2; ++t) {
-            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowBase + t), 2 /* nt */);
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), 2 /* nt */);
             w0[t] = make_uint4(q.x, q.y, q.z, q.w);
         }
 #pragma unroll
@@ -649,15 +667,20 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
     auto row = [&](auto uc, int base) {
         constexpr int v = decltype(uc)::value;
         const int i = base + v;  // iteration = output row y0 + i
-        const int yy = y0 + i;
-        if (yy >= y1)
+        if (i >= nRows)
             return;  // past the band end (uniform)
+        const int yy = dir > 0 ? y0 + i : y1 - 1 - i;
         // DMA(i) retired: after it come 2 DMAs per later iteration (K-2 of them) and the
         // K-1 stores of iterations i-K+1 .. i-1
         wait_vmcnt<3 * K - 5>();
         uint4 n0, n1;
         read_iter(i, n0, n1);
         dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
+#ifdef IQO_EXP_MEMONLY  // timing experiment: memory stream only (wrong output)
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{n0.x ^ n1.y, n0.z ^ n1.w}, dstR, stoff, (yy - a.io.dstRow0) * dstSt,
+                                              IQO_SYM_STORE_AUX);
+        return;
+#endif
         unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
         unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
 
@@ -712,7 +735,7 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, IQO_SYM_STORE_AUX);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every 64 rows and at the band end one pass divides them, one row per lane
@@ -721,13 +744,272 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
                 edgeSum[wib][0][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
             if (edgeR && laneR)
                 edgeSum[wib][1][slot] = make_int4(sum[4], sum[5], sum[6], sum[7]);
-            if (slot == 63 || yy == y1 - 1) {
+            if (slot == 63 || i == nRows - 1) {
                 __builtin_amdgcn_wave_barrier();
-                flush_edges(yy - slot, slot + 1);  // after this row's main store (same addresses)
+                flush_edges(yy - dir * slot, slot + 1);  // after this row's main store (same addresses)
             }
         }
     };
-    for (int base = 0; y0 + base < y1; base += H)
+    for (int base = 0; base < nRows; base += H)
+        static_for<H>([&](auto uc) { row(uc, base); });
+
+    wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
+}
+
+// ================================================================ block-shared symmetric streamer
+//
+// lanczos_sym_kernel with the source rows shared by the waves of a row band: one WORKGROUP = one
+// row band of one frame, wave w = column strip w.  The per-wave rings above fetch every strip's
+// 16-B halo lanes from HBM a second time -- 992-B strips that start off a 128-B line touch 8-9
+// lines each, +13 % read traffic on C2 (FETCH_SIZE).  Here each row lands ONCE in a shared LDS
+// ring slot, in non-overlapping 1-KiB LDS-DMA chunks (chunk c by wave c mod wpr), and every lane
+// reads its 16 bytes, halo included, from LDS.  Columns right of the image are zero in LDS (the
+// out-of-range lanes of a chunk DMA zeros), and a 16-B zero pad sits left of every ring row.  One
+// s_barrier per output row publishes the row's slot and retires the slot read in the previous
+// row before it is refilled.  Waves with fewer chunks than CPW DMA into a sink so the vm-counter
+// pattern is the same in every wave.
+
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+__global__ __launch_bounds__(256) void lanczos_symb_kernel(LanczosArgs a)
+{
+    constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
+    static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
+    static_assert(K >= 2 && CPW >= 1, "ring depth");
+    constexpr int WAIT = 1 + (K - 2) * (2 * CPW + 1);  // vm ops issued after this wave's DMA(i)
+    constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
+    constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
+    static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
+    // LDS: ring [K slots][2 rows][rowPitch] | edgeSum int4 [2][64] | 1 KiB DMA sink
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int rowPitch = a.rowPitch, slotBytes = 2 * rowPitch;
+    uint8_t *const ring = lds;
+    int4 (*const edgeSum)[64] = reinterpret_cast<int4 (*)[64]>(lds + K * slotBytes);
+    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + 2 * 64 * 16);
+
+    const LanczosDev &L = a.l;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const int wpr = a.wavesPerRow;                 // = waves of this workgroup
+    const int band = static_cast<int>(blockIdx.x), wcol = wib;
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;  // whole workgroup
+
+    const int np = a.np, opw = 8 * np;
+    const int x0 = max(0, min(wcol * opw, L.dstW - opw));
+    const int cb = 2 * x0 - 16 + 16 * lane;
+    const int outX = x0 + (lane - 1) * 8;
+    const bool produce = lane >= 1 && lane <= np && outX < L.dstW;
+    const int voff = (lane <= np + 1 && cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;  // prologue loads
+    const int ldsCol = lane <= np + 1 ? 16 + cb : 0;  // this lane's 16 bytes in an LDS ring row
+    const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
+    const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0;
+    const int dbg = a.dbg;
+    const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
+    const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
+    // Odd bands walk bottom-up: a band boundary's halo rows are then read by both bands at the
+    // same time (both at their start or both at their end) and the second read hits the
+    // Infinity Cache instead of HBM.  The window arithmetic is symmetric, so only the row order
+    // changes: walk index t of iteration i is source row rowAt(i, t).
+    const int dir = ((band & 1) && !(dbg & 32)) ? -1 : 1;
+    const int rFirst = 2 * y0 + L.offY;                 // first source row the band reads
+    const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;  // last source row the band reads
+    const int nRows = y1 - y0;
+    const uint32_t bias = opaque(1u << 19);            // rounding bias (VOP3P src2 of the first dot)
+
+    // shared LDS ring: iteration i's two walk rows live in slot i mod K; chunk c (1 KiB of
+    // source columns [1024c, 1024c + 1024) at LDS column 16 + 1024c) is DMA'd by wave c mod wpr
+    const uint32_t ldsBase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint8_t *)lds));
+    const uint8_t *ringLane = ring + ldsCol;
+    auto row_soff = [&](int r) { return (r >= rFirst && r <= rLast) ? (r - srcRow0) * srcSt : 0x7ff00000; };
+    // iteration i (output row y0 + i, or y1 - 1 - i walking up) brings walk rows NY-2 and NY-1
+    auto rowAt = [&](int i, int t) { return dir > 0 ? rFirst + 2 * i + t : rLast - 2 * i - t; };
+    auto dma_iter = [&](int i) {
+        const uint32_t s = ldsBase + static_cast<uint32_t>((i % K) * slotBytes);
+        const int r = rowAt(i, NY - 2);
+#pragma unroll
+        for (int j = 0; j < CPW; ++j) {
+            const int c = wcol + j * wpr;
+            const bool real = c < a.chunks;  // uniform; otherwise a same-count DMA into the sink
+            const int col = 1024 * c + 16 * lane;
+            const int v = (real && col < L.srcW && !(dbg & 2)) ? col : 0x7ff00000;
+            const uint32_t d0 = real ? s + 16 + 1024 * c : ldsBase + sinkLds;
+            const uint32_t d1 = real ? d0 + rowPitch : d0;
+            dma_row(d0, v, srcR, row_soff(r));
+            dma_row(d1, v, srcR, row_soff(r + dir));
+        }
+    };
+    auto read_iter = [&](int i, uint4 &r0, uint4 &r1) {
+        const uint8_t *p = ringLane + (i % K) * slotBytes;
+        r0 = *reinterpret_cast<const uint4 *>(p);
+        r1 = *reinterpret_cast<const uint4 *>(p + rowPitch);
+    };
+
+    // odd-aligned u16 pairs Q_1..Q_8 of one row: (b1,b2) (b3,b4) ... (b15,b16), b16 = right
+    // neighbour's byte 0
+    auto unpack_odd = [&](uint4 v, uint32_t (&q)[8]) {
+        const uint32_t r = static_cast<uint32_t>(
+            __builtin_amdgcn_mov_dpp(static_cast<int>(v.x), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        q[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c020c01u);
+        q[1] = __builtin_amdgcn_perm(v.y, v.x, 0x0c040c03u);
+        q[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c020c01u);
+        q[3] = __builtin_amdgcn_perm(v.z, v.y, 0x0c040c03u);
+        q[4] = __builtin_amdgcn_perm(0u, v.z, 0x0c020c01u);
+        q[5] = __builtin_amdgcn_perm(v.w, v.z, 0x0c040c03u);
+        q[6] = __builtin_amdgcn_perm(0u, v.w, 0x0c020c01u);
+        q[7] = __builtin_amdgcn_perm(r, v.w, 0x0c040c03u);
+    };
+
+    // Border columns of rows [yb, yb + n) from the parked sums: floor(max(S, 0) / D) with the
+    // exact multiply-high constants of plan.cpp magic_x (identity for the interior columns of the
+    // edge lane), clamped to a byte, one dword per row and side -- stored after the row's main
+    // store, so it overwrites those 4 bytes.
+    auto flush_edges = [&](int yb, int n) {
+        auto fix = [&](int sv, int k) {
+            const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.xM[k]) >> L.xT[k];
+            return min(qq, 255u);
+        };
+        const int rowOff = (yb + dir * lane - a.io.dstRow0) * dstSt;
+        if (edgeL) {
+            const int4 e = edgeSum[0][lane & 63];
+            const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff : 0x7ff00000, 0, 0);
+        }
+        if (edgeR) {
+            const int4 e = edgeSum[1][lane & 63];
+            const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff + L.dstW - 4 : 0x7ff00000,
+                                                  0, 0);
+        }
+    };
+
+    // window: at iteration i the NY walk rows rowAt(i, t) (t < NY) live in slots (2i + t) mod NY;
+    // iteration i brings the last two (t = NY-2, NY-1)
+    uint32_t win[NY][8];
+    {
+        // walk rows 0 .. NY-3 of iteration 0 go straight to VGPRs (window slots 0 .. NY-3)
+        uint4 w0[NY - 2];
+#pragma unroll
+        for (int t = 0; t < NY - 2; ++t) {
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), 2 /* nt */);
+            w0[t] = make_uint4(q.x, q.y, q.z, q.w);
+        }
+#pragma unroll
+        for (int t = 0; t < NY - 2; ++t)
+            unpack_odd(w0[t], win[t]);
+    }
+    // zero pad left of every ring row (the left halo lane of the first strip reads it)
+    for (int r = static_cast<int>(threadIdx.x); r < 2 * K; r += static_cast<int>(blockDim.x))
+        *reinterpret_cast<uint4 *>(ring + r * rowPitch) = make_uint4(0u, 0u, 0u, 0u);
+    // ring prologue: DMA(0) .. DMA(K-2), each followed by a dropped store, so that from the first
+    // iteration on the vm counter sees the steady-state order DMA(j), S(j-K+1)
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) {
+        dma_iter(j);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, 0x7ff00000, 0, 0);
+    }
+
+    auto row = [&](auto uc, int base) {
+        constexpr int v = decltype(uc)::value;
+        const int i = base + v;  // iteration = output row y0 + i
+        if (i >= nRows)
+            return;  // past the band end (uniform)
+        const int yy = dir > 0 ? y0 + i : y1 - 1 - i;
+        // this wave's DMA(i) retired: after it come the store of iteration i-K+1 and the 2*CPW
+        // DMAs + 1 store of each of iterations i-K+2 .. i-1; then the workgroup barrier makes
+        // every wave's chunks of iteration i visible and retires all reads of slot (i-1) mod K
+        wait_vmcnt<WAIT>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        uint4 n0, n1;
+        read_iter(i, n0, n1);
+        dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
+#ifdef IQO_EXP_MEMONLY  // timing experiment: memory stream only (wrong output)
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{n0.x ^ n1.y, n0.z ^ n1.w}, dstR, stoff, (yy - a.io.dstRow0) * dstSt,
+                                              IQO_SYM_STORE_AUX);
+        return;
+#endif
+        unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
+        unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
+
+        // vertical: pair p = slots (2v + p, 2v + NY - 1 - p) mod NY
+        uint32_t acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t p0 = win[(2 * v) % NY][c] + win[(2 * v + NY - 1) % NY][c];
+            acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
+        }
+#pragma unroll
+        for (int p = 1; p < H; ++p)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
+                acc[c] = pk_mad(pp, L.cy[p], acc[c]);
+            }
+        if ((yy < L.mainBeginY || yy >= L.mainEndY) && !(dbg & 8)) {
+            // border row (uniform, rare): rows outside the image were read as zero
+            const bool top = yy < L.mainBeginY;
+            const int bi = top ? yy : yy - L.mainEndY;
+            const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
+            const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c] = ydiv2(acc[c], m, sh);
+        }
+
+        // Q_j for j in [JLO, JHI): own pairs 1..8, neighbours' by DPP
+        uint32_t q[JHI - JLO];
+#pragma unroll
+        for (int j = JLO; j < JHI; ++j) {
+            if (j <= 0)
+                q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
+                    static_cast<int>(acc[j + 7]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+            else if (j >= 9)
+                q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
+                    static_cast<int>(acc[j - 9]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+            else
+                q[j - JLO] = acc[j - 1];
+        }
+        int sum[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            int sacc;  // VOP3P form: the bias VGPR is src2, no copy into the accumulator
+            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[0]), "v"(q[k]), "v"(bias));
+#pragma unroll
+            for (int p = 1; p < NX / 2; ++p)
+                sacc = sdot2(q[k + p], L.cxo[p], sacc);
+            sum[k] = sacc;
+        }
+        u32x2 o;
+        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, IQO_SYM_STORE_AUX);
+        if (edgeL || edgeR) {
+            // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
+            // LDS; every 64 rows and at the band end one pass divides them, one row per lane
+            const int slot = i & 63;
+            if (edgeL && laneL)
+                edgeSum[0][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+            if (edgeR && laneR)
+                edgeSum[1][slot] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+            if (slot == 63 || i == nRows - 1) {
+                __builtin_amdgcn_wave_barrier();
+                flush_edges(yy - dir * slot, slot + 1);  // after this row's main store (same addresses)
+            }
+        }
+    };
+    for (int base = 0; base < nRows; base += H)
         static_for<H>([&](auto uc) { row(uc, base); });
 
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
@@ -972,6 +1254,63 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 
 // ================================================================ launchers
 
+namespace {
+
+// Waves of `kernel` (256-thread blocks) resident on the whole current device: occupancy x CUs.
+// Host-side query, cached per kernel.
+int resident_waves(const void *kernel, int block = 256, int ldsBytes = 0)
+{
+    static std::mutex mu;
+    static std::unordered_map<const void *, int> cache;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    // per device and geometry too
+    const void *key = static_cast<const char *>(kernel) + dev + 16 * block + 65536 * ldsBytes;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end())
+            return it->second;
+    }
+    int perCu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCu, kernel, block, static_cast<size_t>(ldsBytes)) !=
+            hipSuccess ||
+        perCu <= 0)
+        perCu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        cus = 256;
+    const int waves = perCu * (block / 64) * cus;
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = waves;
+    return waves;
+}
+
+// Row bands per frame for a band-walking kernel: minimise the makespan in rows walked,
+// (waves in flight rounds) x (rows per band + halo rows re-read at every band start), so that
+// the grid fills whole rounds of the resident waves instead of leaving a straggler round.
+int choose_bands(int rows, int frames, int wavesPerRow, int resident, int halo)
+{
+    int best = 1;
+    int64_t bestCost = INT64_MAX;
+    for (int b = 1; b <= std::min(rows, 512); ++b) {
+        const int rpb = (rows + b - 1) / b;
+        const int bb = (rows + rpb - 1) / rpb;
+        if (bb != b)
+            continue;
+        const int64_t waves = static_cast<int64_t>(frames) * wavesPerRow * bb;
+        const int64_t rounds = (waves + resident - 1) / resident;
+        const int64_t cost = rounds * (rpb + halo);
+        if (cost < bestCost) {
+            bestCost = cost;
+            best = bb;
+        }
+    }
+    return best;
+}
+
+} // namespace
+
+
 hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
@@ -996,9 +1335,6 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
     const int rows = rowEnd - rowBegin;
-    bands = max(1, min(bands, rows));
-    const int rpb = (rows + bands - 1) / bands;
-    bands = (rows + rpb - 1) / rpb;
     int opw = 62 * (16 / l.KX);
     int wpr = (l.dstW + opw - 1) / opw;
     int np = 62;
@@ -1012,7 +1348,57 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
         opw = 8 * np;
         wpr = (l.dstW + opw - 1) / opw;
     }
-    LanczosArgs a{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np};
+    // the instantiation this call runs
+    const int pd = l.prefetch;
+    const void *kern = nullptr;
+    int block = 256, ldsBytes = 0;
+    const int chunks = (l.srcW + 16 + 1023) / 1024;
+    const int cpw = (chunks + wpr - 1) / wpr;
+    const int rowPitch = 16 + 1024 * chunks;
+    const bool shared = l.sym && l.sym != 2 && wpr <= 4 && cpw <= 2;
+    if (shared) {
+        // block-shared ring (default): one workgroup of wpr waves per row band
+        const bool one = (l.cy[0] & 0xffffu) == 1u;
+        const int K = pd <= 2 ? 3 : 4;
+        ldsBytes = K * 2 * rowPitch + 2 * 64 * 16 + 1024;
+        block = 64 * wpr;
+#define IQO_SYMB(NY_, NX_, OX_, ONE_)                                                                   \
+    (K == 3 ? (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 3, 1, ONE_>)  \
+                        : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 3, 2, ONE_>)) \
+            : (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 4, 1, ONE_>)  \
+                        : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 4, 2, ONE_>)))
+        if (l.NY == 10 && one)
+            kern = IQO_SYMB(10, 12, -5, true);
+        else if (l.NY == 10)
+            kern = IQO_SYMB(10, 12, -5, false);
+        else
+            kern = IQO_SYMB(8, 8, -3, false);
+#undef IQO_SYMB
+    } else if (l.sym) {
+        const bool one = (l.cy[0] & 0xffffu) == 1u;
+        if (l.NY == 10 && one)
+            kern = pd <= 2 ? reinterpret_cast<const void *>(lanczos_sym_kernel<10, 12, -5, 3, true>)
+                           : reinterpret_cast<const void *>(lanczos_sym_kernel<10, 12, -5, 4, true>);
+        else if (l.NY == 10)
+            kern = reinterpret_cast<const void *>(lanczos_sym_kernel<10, 12, -5, 4, false>);
+        else
+            kern = pd <= 2 ? reinterpret_cast<const void *>(lanczos_sym_kernel<8, 8, -3, 3, false>)
+                           : reinterpret_cast<const void *>(lanczos_sym_kernel<8, 8, -3, 4, false>);
+    } else if (l.NY == 10) {
+        kern = pd <= 1   ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 10, 14, -3, 1>)
+               : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 10, 14, -3, 2>)
+                         : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 10, 14, -3, 3>);
+    } else {
+        kern = pd <= 1   ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 1>)
+               : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 2>)
+                         : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 3>);
+    }
+    if (bands <= 0)
+        bands = choose_bands(rows, io.frames, wpr, resident_waves(kern, block, ldsBytes), l.NY - 2);
+    bands = max(1, min(bands, rows));
+    const int rpb = (rows + bands - 1) / bands;
+    bands = (rows + rpb - 1) / rpb;
+    LanczosArgs a{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks};
     // buffer ranges: the source window spans rows [srcRow0, srcH) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(l.srcH - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -1023,41 +1409,10 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
-    dim3 grid(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
-    const int pd = l.prefetch;
-    if (l.sym) {
-        const bool one = (l.cy[0] & 0xffffu) == 1u;
-        if (l.NY == 10 && one) {
-            if (pd <= 2)
-                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 3, true>), grid, dim3(256), 0, s, a);
-            else
-                hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 4, true>), grid, dim3(256), 0, s, a);
-        } else if (l.NY == 10) {
-            hipLaunchKernelGGL((lanczos_sym_kernel<10, 12, -5, 4, false>), grid, dim3(256), 0, s, a);
-        } else {
-            if (pd <= 2)
-                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 3, false>), grid, dim3(256), 0, s, a);
-            else
-                hipLaunchKernelGGL((lanczos_sym_kernel<8, 8, -3, 4, false>), grid, dim3(256), 0, s, a);
-        }
-        return hipGetLastError();
-    }
-    if (l.NY == 10) {
-        if (pd <= 1)
-            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 1>), grid, dim3(256), 0, s, a);
-        else if (pd == 2)
-            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 2>), grid, dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 10, 14, -3, 3>), grid, dim3(256), 0, s, a);
-    } else {
-        if (pd <= 1)
-            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2, 1>), grid, dim3(256), 0, s, a);
-        else if (pd == 2)
-            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2, 2>), grid, dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL((lanczos_stream_kernel<2, 2, 8, 10, -2, 3>), grid, dim3(256), 0, s, a);
-    }
-    return hipGetLastError();
+    const dim3 grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
+                             : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, grid, dim3(static_cast<unsigned>(block)), args, static_cast<size_t>(ldsBytes), s);
 }
 
 hipError_t launch_area_int(const AreaDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
@@ -1088,14 +1443,26 @@ hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int
     if (g.srcW % 8 || g.dstW != 2 * g.srcW || g.srcW < 8)
         return hipErrorInvalidValue;
     const int rows = rowEnd - rowBegin;
-    bands = max(1, min(bands, rows));
-    const int rpb = (rows + bands - 1) / bands;
-    bands = (rows + rpb - 1) / rpb;
     // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
     const int lanes = g.srcW / 8;
     int wpr = (lanes + 61) / 62;
     int np = (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
+    // nontemporal stores by default (dbg 16 = plain stores, for A/B); 2 rows in flight per wave
+    // measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
+    const bool nt = !(g.dbg & 16);
+    const int pd = g.prefetch == 0 ? 2 : g.prefetch;
+    const void *kern = pd >= 8 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<8, true>)
+                                     : reinterpret_cast<const void *>(linear_up2_kernel<8, false>))
+                       : pd >= 4 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<4, true>)
+                                       : reinterpret_cast<const void *>(linear_up2_kernel<4, false>))
+                                 : (nt ? reinterpret_cast<const void *>(linear_up2_kernel<2, true>)
+                                       : reinterpret_cast<const void *>(linear_up2_kernel<2, false>));
+    if (bands <= 0)
+        bands = choose_bands(rows, io.frames, wpr, resident_waves(kern), 2);
+    bands = max(1, min(bands, rows));
+    const int rpb = (rows + bands - 1) / bands;
+    bands = (rows + rpb - 1) / rpb;
     LinearArgs a{g, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, np};
     const int64_t sb = static_cast<int64_t>(g.srcH - io.srcRow0 - 1) * io.srcSt + g.srcW;
     const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + g.dstW;
@@ -1105,18 +1472,8 @@ hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
     dim3 grid(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
-    // nontemporal stores by default (dbg 16 = plain stores, for A/B); 2 rows in flight per wave
-    // measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
-    const bool nt = !(g.dbg & 16);
-    const int pd = g.prefetch == 0 ? 2 : g.prefetch;
-    auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, dim3(256), 0, s, a); };
-    if (pd >= 8)
-        nt ? go(linear_up2_kernel<8, true>) : go(linear_up2_kernel<8, false>);
-    else if (pd >= 4)
-        nt ? go(linear_up2_kernel<4, true>) : go(linear_up2_kernel<4, false>);
-    else
-        nt ? go(linear_up2_kernel<2, true>) : go(linear_up2_kernel<2, false>);
-    return hipGetLastError();
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, grid, dim3(256), args, 0, s);
 }
 
 } // namespace iqo_amd

@@ -167,15 +167,16 @@ STREAM_SHAPES = [
 
 @pytest.mark.parametrize("shape", STREAM_SHAPES, ids=lambda s: "L%d_%dx%d" % s[:3])
 def test_stream_variants_agree_with_oracle(shape):
-    """Both Lanczos streamers (symmetric window and accumulator ring), every prefetch depth, forced
-    lane counts and band splits produce the oracle's output."""
+    """Every Lanczos streamer (block-shared symmetric, accumulator ring, per-wave symmetric), every
+    prefetch depth, forced lane counts and band splits produce the oracle's output."""
     d, sw, sh, dw, dh = shape
     frames = _noise_batch(2, sw, sh, 300)
     frames[1, :, : sw // 5] = 255
     src = torch.from_numpy(frames).to(DEV)
     exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 1, frames[f]) for f in range(2)]
     for variant, pd, lanes, bands in [(0, 1, 0, 0), (0, 2, 0, 7), (0, 3, 0, 0), (0, 2, 62, 3), (0, 3, 33, 0),
-                                      (1, 3, 0, 0), (1, 1, 0, 5)]:
+                                      (0, 3, 0, 1), (1, 3, 0, 0), (1, 1, 0, 5), (2, 3, 0, 0), (2, 1, 0, 5),
+                                      (2, 2, 40, 0)]:
         r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
         assert r.describe()["kernel"] == "lanczos_stream"
         r.set_option("stream_variant", variant)
