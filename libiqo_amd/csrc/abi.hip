@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -38,9 +39,6 @@ struct iqo_hip_plan {
                             // streamer, 2: per-wave symmetric streamer
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int chunkFrames = 0;    // frames per launch (0 = auto: about kChunkBytes of frames)
-    hipStream_t stream = nullptr;
-    uint8_t *stageSrc = nullptr, *stageDst = nullptr;
-    size_t stageSrcCap = 0, stageDstCap = 0;
 };
 
 namespace {
@@ -66,6 +64,111 @@ private:
     int prev_ = 0;
     bool ok_ = false;
 };
+
+// ---- host-pointer path (iqo_hip_resize): staging pool
+//
+// Device staging frames, pinned host staging, three streams (H2D, kernels, D2H) and per-band
+// events, pooled per device for the whole process: constructing a resizer stays cheap (the
+// reference benchmark constructs one per call, benchmark.cpp:215-226), and one staging set is
+// borrowed per call, so distinct plans can run concurrently from different threads.  The pool
+// is never torn down (the HIP runtime may already be gone at static destruction).
+constexpr int kHostBands = 8;      // output-row bands of the host-pointer pipeline
+constexpr int kHostBandRows = 64;  // ... each at least this tall
+
+struct HostStage {
+    int device = 0;
+    hipStream_t sIn = nullptr, sK = nullptr, sOut = nullptr;
+    hipEvent_t evIn[kHostBands] = {}, evK[kHostBands] = {}, evOut[kHostBands] = {};
+    uint8_t *dSrc = nullptr, *dDst = nullptr, *hSrc = nullptr, *hDst = nullptr;
+    size_t dSrcCap = 0, dDstCap = 0, hSrcCap = 0, hDstCap = 0;
+};
+
+std::mutex g_stageMu;
+std::vector<HostStage *> g_stagePool;
+
+HostStage *acquire_stage(int device)
+{
+    {
+        std::lock_guard<std::mutex> g(g_stageMu);
+        for (size_t i = 0; i < g_stagePool.size(); ++i)
+            if (g_stagePool[i]->device == device) {
+                HostStage *st = g_stagePool[i];
+                g_stagePool.erase(g_stagePool.begin() + static_cast<std::ptrdiff_t>(i));
+                return st;
+            }
+    }
+    HostStage *st = new (std::nothrow) HostStage();
+    if (!st)
+        return nullptr;
+    st->device = device;
+    bool ok = hipStreamCreateWithFlags(&st->sIn, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&st->sK, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&st->sOut, hipStreamNonBlocking) == hipSuccess;
+    for (int b = 0; ok && b < kHostBands; ++b)
+        ok = hipEventCreateWithFlags(&st->evIn[b], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&st->evK[b], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&st->evOut[b], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        // keep what was created: the set is still returned to the pool and retried next time
+        std::lock_guard<std::mutex> g(g_stageMu);
+        g_stagePool.push_back(st);
+        return nullptr;
+    }
+    return st;
+}
+
+void release_stage(HostStage *st)
+{
+    std::lock_guard<std::mutex> g(g_stageMu);
+    g_stagePool.push_back(st);
+}
+
+int grow_device(uint8_t **p, size_t *cap, size_t bytes)
+{
+    if (bytes <= *cap)
+        return IQO_HIP_OK;
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(reinterpret_cast<void **>(p), bytes) != hipSuccess)
+        return IQO_HIP_ENOMEM;
+    *cap = bytes;
+    return IQO_HIP_OK;
+}
+
+int grow_pinned(uint8_t **p, size_t *cap, size_t bytes)
+{
+    if (bytes <= *cap)
+        return IQO_HIP_OK;
+    (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipHostMalloc(reinterpret_cast<void **>(p), bytes, hipHostMallocDefault) != hipSuccess)
+        return IQO_HIP_ENOMEM;
+    *cap = bytes;
+    return IQO_HIP_OK;
+}
+
+// Host memory the DMA engines reach directly: hipHostMalloc'd or hipHostRegister'ed.
+bool is_pinned_host(const void *p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error here; clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+void copy_rows(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, size_t w, size_t rows)
+{
+    if (dstSt == w && srcSt == w) {
+        std::memcpy(dst, src, w * rows);
+        return;
+    }
+    for (size_t r = 0; r < rows; ++r)
+        std::memcpy(dst + r * dstSt, src + r * srcSt, w);
+}
 
 bool is_gfx950(int dev)
 {
@@ -142,10 +245,6 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dChunks);
     (void)hipFree(h->dTabX);
     (void)hipFree(h->dTabY);
-    (void)hipFree(h->stageSrc);
-    (void)hipFree(h->stageDst);
-    if (h->stream)
-        (void)hipStreamDestroy(h->stream);
     delete h;
 }
 
@@ -482,6 +581,80 @@ int iqo_hip_resize_band(iqo_hip_plan *h, size_t nFrames, size_t dstRow0, size_t 
                     dDstBand, static_cast<hipStream_t>(stream));
 }
 
+// The host-pointer drop-in (reference resize(), LanczosResizer.hpp:47-52 semantics: synchronous,
+// host buffers).  Output-row bands are pipelined over three streams: band b's new source rows go
+// up on sIn, its kernel runs on sK once they have landed, its output rows come down on sOut, so
+// the H2D of band b+1, the kernel of band b and the D2H of band b-1 overlap (PCIe is full
+// duplex).  Pinned host buffers are DMA'd in place; pageable ones are staged through pinned
+// memory by the calling thread one band ahead of the copy engines.
+static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
+{
+    const Plan &p = h->p;
+    const size_t W = static_cast<size_t>(p.srcW), w = static_cast<size_t>(p.dstW);
+    const size_t sPitch = (W + 15) & ~size_t(15);
+    const size_t dPitch = (w + 15) & ~size_t(15);
+    const size_t sBytes = sPitch * p.srcH, dBytes = dPitch * p.dstH;
+    if (grow_device(&st->dSrc, &st->dSrcCap, sBytes) || grow_device(&st->dDst, &st->dDstCap, dBytes))
+        return IQO_HIP_ENOMEM;
+    const bool pinSrc = is_pinned_host(src), pinDst = is_pinned_host(dst);
+    if (!pinSrc && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
+        return IQO_HIP_ENOMEM;
+    if (!pinDst && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
+        return IQO_HIP_ENOMEM;
+
+    const int dstH = p.dstH;
+    const int bands = std::max(1, std::min(kHostBands, dstH / kHostBandRows));
+    auto bandRow = [&](int b) { return static_cast<int>(static_cast<int64_t>(dstH) * b / bands); };
+    int rowsUp = 0;  // source rows [0, rowsUp) are queued for upload
+    for (int b = 0; b < bands; ++b) {
+        const int r0 = bandRow(b), r1 = bandRow(b + 1);
+        int s0, s1;
+        iqo_amd::band_src_rows(p, r0, r1, &s0, &s1);
+        if (b == bands - 1)
+            s1 = p.srcH;
+        if (s1 > rowsUp) {
+            const size_t n = static_cast<size_t>(s1 - rowsUp);
+            const uint8_t *from = src + static_cast<size_t>(rowsUp) * srcSt;
+            size_t fromSt = srcSt;
+            if (!pinSrc) {
+                uint8_t *pin = st->hSrc + static_cast<size_t>(rowsUp) * sPitch;
+                copy_rows(pin, sPitch, from, srcSt, W, n);
+                from = pin;
+                fromSt = sPitch;
+            }
+            if (hipMemcpy2DAsync(st->dSrc + static_cast<size_t>(rowsUp) * sPitch, sPitch, from, fromSt, W, n,
+                                 hipMemcpyHostToDevice, st->sIn) != hipSuccess)
+                return IQO_HIP_EHIP;
+            rowsUp = s1;
+        }
+        if (hipEventRecord(st->evIn[b], st->sIn) != hipSuccess || hipStreamWaitEvent(st->sK, st->evIn[b], 0) != hipSuccess)
+            return IQO_HIP_EHIP;
+        const size_t rows = static_cast<size_t>(r1 - r0);
+        int rc = run_band(h, 1, static_cast<size_t>(r0), rows, 0, sPitch, sBytes, st->dSrc, dPitch, dBytes,
+                          st->dDst + static_cast<size_t>(r0) * dPitch, st->sK);
+        if (rc)
+            return rc;
+        if (hipEventRecord(st->evK[b], st->sK) != hipSuccess || hipStreamWaitEvent(st->sOut, st->evK[b], 0) != hipSuccess)
+            return IQO_HIP_EHIP;
+        uint8_t *to = pinDst ? dst + static_cast<size_t>(r0) * dstSt : st->hDst + static_cast<size_t>(r0) * dPitch;
+        if (hipMemcpy2DAsync(to, pinDst ? dstSt : dPitch, st->dDst + static_cast<size_t>(r0) * dPitch, dPitch, w, rows,
+                             hipMemcpyDeviceToHost, st->sOut) != hipSuccess ||
+            hipEventRecord(st->evOut[b], st->sOut) != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
+    // output bands leave the pinned staging as they land
+    for (int b = 0; b < bands; ++b) {
+        if (hipEventSynchronize(st->evOut[b]) != hipSuccess)
+            return IQO_HIP_EHIP;
+        if (!pinDst) {
+            const int r0 = bandRow(b), r1 = bandRow(b + 1);
+            copy_rows(dst + static_cast<size_t>(r0) * dstSt, dstSt, st->hDst + static_cast<size_t>(r0) * dPitch, dPitch,
+                      w, static_cast<size_t>(r1 - r0));
+        }
+    }
+    return IQO_HIP_OK;
+}
+
 int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
 {
     if (!h || !src || !dst)
@@ -492,38 +665,18 @@ int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dst
     DeviceGuard guard(h->device);
     if (!guard.ok())
         return IQO_HIP_ENODEV;
-    if (!h->stream && hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess)
+    HostStage *st = acquire_stage(h->device);
+    if (!st)
         return IQO_HIP_EHIP;
-    const size_t sPitch = (static_cast<size_t>(p.srcW) + 15) & ~size_t(15);
-    const size_t dPitch = (static_cast<size_t>(p.dstW) + 15) & ~size_t(15);
-    const size_t sBytes = sPitch * p.srcH, dBytes = dPitch * p.dstH;
-    if (sBytes > h->stageSrcCap) {
-        (void)hipFree(h->stageSrc);
-        h->stageSrc = nullptr;
-        h->stageSrcCap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&h->stageSrc), sBytes) != hipSuccess)
-            return IQO_HIP_ENOMEM;
-        h->stageSrcCap = sBytes;
+    int rc = host_resize(h, st, srcSt, src, dstSt, dst);
+    if (rc) {
+        // leave nothing in flight on the staging set before it goes back to the pool
+        (void)hipStreamSynchronize(st->sIn);
+        (void)hipStreamSynchronize(st->sK);
+        (void)hipStreamSynchronize(st->sOut);
     }
-    if (dBytes > h->stageDstCap) {
-        (void)hipFree(h->stageDst);
-        h->stageDst = nullptr;
-        h->stageDstCap = 0;
-        if (hipMalloc(reinterpret_cast<void **>(&h->stageDst), dBytes) != hipSuccess)
-            return IQO_HIP_ENOMEM;
-        h->stageDstCap = dBytes;
-    }
-    if (hipMemcpy2DAsync(h->stageSrc, sPitch, src, srcSt, p.srcW, p.srcH, hipMemcpyHostToDevice, h->stream) != hipSuccess)
-        return IQO_HIP_EHIP;
-    int rc = run_band(h, 1, 0, static_cast<size_t>(p.dstH), 0, sPitch, sBytes, h->stageSrc, dPitch, dBytes,
-                      h->stageDst, h->stream);
-    if (rc)
-        return rc;
-    if (hipMemcpy2DAsync(dst, dstSt, h->stageDst, dPitch, p.dstW, p.dstH, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
-        return IQO_HIP_EHIP;
-    if (hipStreamSynchronize(h->stream) != hipSuccess)
-        return IQO_HIP_EHIP;
-    return IQO_HIP_OK;
+    release_stage(st);
+    return rc;
 }
 
 const char *iqo_hip_strerror(int status)

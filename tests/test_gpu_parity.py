@@ -220,6 +220,31 @@ def test_linear_up2_streamer_variants(shape):
             assert bad.size == 0, (shape, pd, bands, f, bad[:4].tolist())
 
 
+@pytest.mark.parametrize("cfg", CONFIGS[:4], ids=["c2", "c3", "c4", "c1"])
+def test_host_pointer_pipeline_pinned_and_pageable(cfg):
+    """The host-pointer drop-in (band-pipelined H2D / kernel / D2H) gives the oracle's output from
+    pageable numpy buffers and from pinned host tensors, with padded strides, and repeatedly with
+    one plan (the staging set is pooled and reused)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    frame = ol.gen("noise", sw, sh, 21)
+    exp = ol.run_oracle(m, d, sw, sh, dw, dh, px, frame)
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    # pageable, tight strides (twice: the pooled staging set is reused)
+    for _ in range(2):
+        out = np.zeros((dh, dw), np.uint8)
+        r.resize(sw, frame, dw, out)
+        assert (out == exp).all(), cfg
+    # pinned, padded strides
+    sst, dst_st = sw + 32, dw + 48
+    src = torch.zeros((sh, sst), dtype=torch.uint8).pin_memory()
+    src[:, :sw] = torch.from_numpy(frame)
+    out = torch.full((dh, dst_st), 7, dtype=torch.uint8).pin_memory()
+    r.resize(sst, src, dst_st, out)
+    got = out.numpy()
+    assert (got[:, :dw] == exp).all(), cfg
+    assert (got[:, dw:] == 7).all(), "bytes past the row written"
+
+
 @pytest.mark.parametrize("value", [0, 255])
 def test_flat_frames_stay_flat_full_size(value):
     for m, d, sw, sh, dw, dh, px in CONFIGS[:3]:
