@@ -386,6 +386,9 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
                 l.xM[k] = f.xM[k];
                 l.xT[k] = f.xT[k];
             }
+            l.yTopNeg = f.yTopNeg;
+            l.yBotNeg = f.yBotNeg;
+            l.xNeg = f.xNeg;
             l.dbg = h->debugFlags;
             l.prefetch = h->prefetch;
             l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant == 2 ? 2 : 1);

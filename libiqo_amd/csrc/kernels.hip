@@ -415,9 +415,13 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
                 const int bi = top ? yy : yy - L.mainEndY;
                 const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
                 const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
+                const bool neg = ((top ? L.yTopNeg : L.yBotNeg) >> bi) & 1;  // deno < 0 (uniform)
 #pragma unroll
-                for (int c = 0; c < 8; ++c)
+                for (int c = 0; c < 8; ++c) {
                     acc[c] = ydiv2(acc[c], m, sh);
+                    if (neg)  // trunc(n / -d) == -trunc(n / d), per int16 half
+                        acc[c] = __builtin_bit_cast(uint32_t, u16x2{0, 0} - __builtin_bit_cast(u16x2, acc[c]));
+                }
             }
 
             // neighbour work columns by DPP (lane l-1 / l+1), then the horizontal taps
@@ -444,14 +448,16 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
             }
             if (edgeL || edgeR) {
                 // edge wave (uniform): values k < 4 of the left edge lane / k >= 4 of the right
-                // edge lane become floor(max(sum, 0) / D) -- negative border quotients clamp to
-                // 0 like the reference's int16 -> u8 clamp -- re-scaled by 2^20 for the pack
+                // edge lane become min(255, floor(max(+-sum, 0) / |D|)) -- quotients of the wrong
+                // sign clamp to 0 like the reference's int16 -> u8 clamp (the plan guarantees
+                // they fit int16) -- re-scaled by 2^20 for the pack
 #pragma unroll
                 for (int k = 0; k < OUTS; ++k) {
                     const bool side = k < 4 ? edgeL : edgeR;
                     if (side) {
-                        const uint32_t n = static_cast<uint32_t>(max(sum[k], 0));
-                        const uint32_t q = __umulhi(n, L.xM[k]) >> L.xT[k];
+                        const int sv = ((L.xNeg >> k) & 1) ? -sum[k] : sum[k];
+                        const uint32_t n = static_cast<uint32_t>(max(sv, 0));
+                        const uint32_t q = min(__umulhi(n, L.xM[k]) >> L.xT[k], 255u);
                         sum[k] = (k < 4 ? laneL : laneR) ? static_cast<int>(q << 20) : sum[k];
                     }
                 }
@@ -1331,7 +1337,9 @@ hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int r
 
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)
 {
-    return KY == 2 && KX == 2 && ((NY == 10 && NXP == 14 && offX == -6) || (NY == 8 && NXP == 10 && offX == -4));
+    return KY == 2 && KX == 2 &&
+           ((NY == 10 && NXP == 14 && offX == -6) || (NY == 8 && NXP == 10 && offX == -4) ||
+            (NY == 4 && NXP == 4 && offX == 0));
 }
 
 int lanczos_stream_block(int) { return 256; }
@@ -1391,6 +1399,10 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
         else
             kern = pd <= 2 ? reinterpret_cast<const void *>(lanczos_sym_kernel<8, 8, -3, 3, false>)
                            : reinterpret_cast<const void *>(lanczos_sym_kernel<8, 8, -3, 4, false>);
+    } else if (l.NY == 4) {
+        kern = pd <= 1   ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 4, 4, 0, 1>)
+               : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 4, 4, 0, 2>)
+                         : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 4, 4, 0, 3>);
     } else if (l.NY == 10) {
         kern = pd <= 1   ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 10, 14, -3, 1>)
                : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 10, 14, -3, 2>)

@@ -42,6 +42,7 @@ struct LanczosDev {
     // arrive in SGPRs and cost no device table
     uint32_t yTopM[16], yBotM[16], xM[8];
     int yTopS[16], yBotS[16], xT[8];
+    int yTopNeg, yBotNeg, xNeg;  // bit i: border row / column i has a negative denominator
     int dbg;                     // timing experiments only (see kernels.hip)
     int prefetch;                // prefetch depth in output rows (1..3)
     // symmetric streamer (plan.hpp FastLanczos::sym)

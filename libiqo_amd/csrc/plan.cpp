@@ -440,6 +440,14 @@ void pick_fast_lanczos(Plan *p)
     f.NY = hi - lo;
     f.offY = 1 - m + lo;  // first tap row = KY*y + 1 - m + lo  (srcOY = floor(y*KY) + 1)
     f.cy.assign(y.table.begin() + lo, y.table.begin() + hi);
+    // the accumulator ring needs NY % KY == 0: pad with zero taps below (a zero tap adds nothing
+    // to the interior sum nor to the masked border sum; the border divisors come from the
+    // reference coordinates, not from these taps)
+    if (KY > 0 && !y.table.empty())
+        while (f.NY % KY) {
+            f.cy.push_back(0);
+            ++f.NY;
+        }
     // X: drop zero taps, then pad to an even first column and an even tap count (int16 pairs).
     int mx = x.taps / 2, xl = 0, xh = x.taps;
     while (xl < xh && x.table[xl] == 0)
@@ -486,12 +494,21 @@ void pick_fast_lanczos(Plan *p)
         return;
     if (p->dstW % 8 || x.mainBegin > 4 || p->dstW - x.mainEnd > 4 || y.mainBegin > 16 || p->dstH - y.mainEnd > 16)
         return;
-    for (size_t i = 0; i < f.denoYTop.size(); ++i)
-        if (!magic_y(f.denoYTop[i], &f.yTopM[i], &f.yTopS[i]))
+    // negative denominators (a border row / column whose valid taps sum below zero) divide by
+    // the magnitude and flip the sign: C truncation is symmetric
+    f.yTopNeg = f.yBotNeg = f.xNeg = 0;
+    for (size_t i = 0; i < f.denoYTop.size(); ++i) {
+        const int32_t dn = f.denoYTop[i];
+        if (!magic_y(dn < 0 ? -dn : dn, &f.yTopM[i], &f.yTopS[i]))
             return;
-    for (size_t i = 0; i < f.denoYBot.size(); ++i)
-        if (!magic_y(f.denoYBot[i], &f.yBotM[i], &f.yBotS[i]))
+        f.yTopNeg |= dn < 0 ? 1 << i : 0;
+    }
+    for (size_t i = 0; i < f.denoYBot.size(); ++i) {
+        const int32_t dn = f.denoYBot[i];
+        if (!magic_y(dn < 0 ? -dn : dn, &f.yBotM[i], &f.yBotS[i]))
             return;
+        f.yBotNeg |= dn < 0 ? 1 << i : 0;
+    }
     for (int k = 0; k < 8; ++k) {
         const int c = k < 4 ? k : p->dstW - 8 + k;  // column of edge-lane value k
         int64_t D = int64_t(1) << 20;               // identity: floor(s / 2^20) == s >> 20
@@ -499,15 +516,22 @@ void pick_fast_lanczos(Plan *p)
             D = f.dXLeft[static_cast<size_t>(c)];
         else if (k >= 4 && c >= x.mainEnd && c >= 0)
             D = f.dXRight[static_cast<size_t>(c - x.mainEnd)];
+        if (D < 0) {
+            D = -D;
+            f.xNeg |= 1 << k;
+        }
         if (D != (int64_t(1) << 20) && (maxSum / D >= 32768))
             return;  // border quotient must fit int16 (it is int16-cast before the clamp)
         if (!magic_x(D, &f.xM[k], &f.xT[k]))
             return;
     }
     // instantiated shapes (kernels.hip): (KY,KX,NY,NXP,offX/2) = (2,2,10,14,-3) Lanczos-3 2:1,
-    // (2,2,8,10,-2) Lanczos-2 2:1.  Everything else runs the general kernel.
+    // (2,2,8,10,-2) Lanczos-2 2:1, (2,2,4,4,0) the pxScale-2 chroma tables of Lanczos-2/3 2:1
+    // (3 non-zero taps, IQOLanczosResizerImpl_Generic.cpp:144-190 with degFactor).  Everything
+    // else runs the general kernel.
     bool inst = KY == 2 && KX == 2 && ((f.NY == 10 && f.NXP == 14 && f.offX == -6) ||
-                                       (f.NY == 8 && f.NXP == 10 && f.offX == -4));
+                                       (f.NY == 8 && f.NXP == 10 && f.offX == -4) ||
+                                       (f.NY == 4 && f.NXP == 4 && f.offX == 0));
     // symmetric variant: (NY, NX, offXO) = (10, 12, -5) Lanczos-3 2:1, (8, 8, -3) Lanczos-2 2:1
     f.NX = xh - xl;
     f.offXO = off;
@@ -515,7 +539,7 @@ void pick_fast_lanczos(Plan *p)
     bool symY = (f.NY % 2) == 0;
     for (int i = 0; symY && i < f.NY / 2; ++i)
         symY = f.cy[static_cast<size_t>(i)] == f.cy[static_cast<size_t>(f.NY - 1 - i)];
-    f.sym = inst && symY && (off & 1) && ((f.NY == 10 && f.NX == 12 && off == -5) || (f.NY == 8 && f.NX == 8 && off == -3));
+    f.sym = inst && symY && (off & 1) && !f.yTopNeg && !f.yBotNeg && !f.xNeg && ((f.NY == 10 && f.NX == 12 && off == -5) || (f.NY == 8 && f.NX == 8 && off == -3));
     if (!inst || (p->srcW % 16) || p->srcW > 8192)
         return;
     p->kernel = 1;  // IQO_KERNEL_LANCZOS_STREAM

@@ -72,6 +72,9 @@ struct FastLanczos {
     // D = 2^20, for columns of those lanes that are not border columns).
     uint32_t yTopM[16] = {}, yBotM[16] = {}, xM[8] = {};
     int32_t yTopS[16] = {}, yBotS[16] = {}, xT[8] = {};
+    // bit i: border row / column i divides by a negative denominator (the pxScale-2 chroma tables;
+    // accumulator-ring streamer only)
+    int yTopNeg = 0, yBotNeg = 0, xNeg = 0;
 };
 
 // Exact-division constants (exposed for tests): false if the divisor is outside the range the

@@ -189,6 +189,35 @@ def test_stream_variants_agree_with_oracle(shape):
             assert bad.size == 0, (shape, variant, pd, lanes, bands, f, bad[:4].tolist())
 
 
+CHROMA_SHAPES = [
+    (3, 1920, 1080, 960, 540),  # the 4:2:0 chroma planes of C2 (pxScale 2: 3-tap tables, negative
+    (2, 320, 240, 160, 120),    # border denominators) and of C1
+    (3, 1936, 1090, 968, 545),
+    (3, 640, 480, 320, 240),
+    (2, 2064, 40, 1032, 20),
+]
+
+
+@pytest.mark.parametrize("shape", CHROMA_SHAPES, ids=lambda s: "L%d_%dx%d_px2" % s[:3])
+def test_chroma_pxscale2_stream_agrees_with_oracle(shape):
+    """pxScale-2 (chroma) Lanczos tables run the accumulator-ring streamer, including border rows
+    and columns whose valid taps sum to a negative denominator."""
+    d, sw, sh, dw, dh = shape
+    frames = _noise_batch(2, sw, sh, 700)
+    frames[1, sh // 2:, :] = 255
+    src = torch.from_numpy(frames).to(DEV)
+    exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 2, frames[f]) for f in range(2)]
+    for pd, bands in [(1, 0), (2, 3), (3, 0), (3, dh)]:
+        r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 2)
+        assert r.describe()["kernel"] == "lanczos_stream"
+        r.set_option("prefetch", pd)
+        r.set_option("bands", bands)
+        out = r.resize_tensor(src).cpu().numpy()
+        for f in range(2):
+            bad = np.argwhere(out[f] != exp[f])
+            assert bad.size == 0, (shape, pd, bands, f, bad[:4].tolist())
+
+
 LINEAR_UP2_SHAPES = [
     (1920, 1080),  # C4: 4 waves x 60 lanes per row
     (640, 480),    # 80 lanes: 2 waves x 40
