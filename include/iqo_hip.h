@@ -106,6 +106,29 @@ int iqo_hip_resize_band(iqo_hip_plan *plan, size_t nFrames, size_t dstRow0, size
                         size_t srcRow0, size_t srcSt, size_t srcFrameSt, const uint8_t *dSrcWindow,
                         size_t dstSt, size_t dstFrameSt, uint8_t *dDstBand, void *stream);
 
+/* ---- YUV 4:2:0 (I420) three-plane resize: the reference benchmark's workload
+ * (benchmark/benchmark.cpp:131-229, sample/resize_yuv420p.cpp:121-163): Y srcW x srcH -> dstW x dstH,
+ * U and V srcW/2 x srcH/2 -> dstW/2 x dstH/2 with the same method; Lanczos chroma uses pxScale 2.
+ * The reference composes three resizer objects; here one plan holds the luma and chroma plans. */
+typedef struct iqo_hip_yuv_plan iqo_hip_yuv_plan;
+int iqo_hip_plan_yuv420(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
+                        int device, iqo_hip_yuv_plan **out);
+void iqo_hip_yuv_plan_destroy(iqo_hip_yuv_plan *plan);
+/* Plane 0 = the luma plan, 1 = the chroma plan (for iqo_hip_plan_set_option / _query). */
+iqo_hip_plan *iqo_hip_yuv_plane(iqo_hip_yuv_plan *plan, int plane);
+/* Device-resident batch, asynchronous on `stream`: frame f's planes start at srcY/srcU/srcV +
+ * f*srcFrameSt (likewise dst).  All three planes go in ONE launch when the plane kernels have a
+ * fused instantiation (*fused = 1; the fast kernels of every BASELINE shape do), else one launch
+ * per plane (*fused = 0).  `fused` may be NULL. */
+int iqo_hip_resize_yuv420_device(iqo_hip_yuv_plan *plan, size_t nFrames, size_t srcStY, size_t srcStUV,
+                                 size_t srcFrameSt, const uint8_t *srcY, const uint8_t *srcU, const uint8_t *srcV,
+                                 size_t dstStY, size_t dstStUV, size_t dstFrameSt, uint8_t *dstY, uint8_t *dstU,
+                                 uint8_t *dstV, void *stream, int *fused);
+/* Host pointers, synchronous: the three planes through the pipelined host path of iqo_hip_resize. */
+int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *plan, size_t srcStY, const uint8_t *srcY, size_t srcStUV,
+                          const uint8_t *srcU, const uint8_t *srcV, size_t dstStY, uint8_t *dstY, size_t dstStUV,
+                          uint8_t *dstU, uint8_t *dstV);
+
 const char *iqo_hip_strerror(int status);
 const char *iqo_hip_version(void);
 

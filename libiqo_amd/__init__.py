@@ -70,6 +70,14 @@ def lib():
     L.iqo_host_kernel_for.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz]
     L.iqo_host_band_src_rows.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz,
                                          ctypes.POINTER(_c_sz), ctypes.POINTER(_c_sz)]
+    L.iqo_hip_plan_yuv420.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, ctypes.c_int, pp]
+    L.iqo_hip_yuv_plan_destroy.argtypes = [_vp]
+    L.iqo_hip_yuv_plan_destroy.restype = None
+    L.iqo_hip_yuv_plane.argtypes = [_vp, ctypes.c_int]
+    L.iqo_hip_yuv_plane.restype = _vp
+    L.iqo_hip_resize_yuv420_device.argtypes = [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _vp, _vp, _c_sz, _c_sz, _c_sz,
+                                               _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_int)]
+    L.iqo_hip_resize_yuv420.argtypes = [_vp, _c_sz, _vp, _c_sz, _vp, _vp, _c_sz, _vp, _c_sz, _vp, _vp]
     _lib = L
     return L
 
@@ -232,3 +240,56 @@ def make_resizer(method, degree, srcW, srcH, dstW, dstH, pxScale=1, device=None)
     if method == "linear":
         return LinearResizer(srcW, srcH, dstW, dstH, device)
     raise ValueError(method)
+
+
+class Yuv420Resizer:
+    """I420 three-plane resizer: the reference benchmark's workload (benchmark.cpp:131-229), Y at
+    full size and U, V at half size with the same method (Lanczos chroma: pxScale 2)."""
+
+    def __init__(self, method, degree, srcW, srcH, dstW, dstH, device=None):
+        self.method, self.degree = method, int(degree)
+        self.srcW, self.srcH, self.dstW, self.dstH = int(srcW), int(srcH), int(dstW), int(dstH)
+        self.device = 0 if device is None else int(device)
+        self._plan = _vp()
+        _check(lib().iqo_hip_plan_yuv420(_METHODS[method], self.degree, self.srcW, self.srcH, self.dstW, self.dstH,
+                                         self.device, ctypes.byref(self._plan)), "Yuv420Resizer")
+
+    def __del__(self):
+        p = getattr(self, "_plan", None)
+        if p and _lib is not None:
+            _lib.iqo_hip_yuv_plan_destroy(p)
+            self._plan = _vp()
+
+    def set_option(self, key, value, plane=None):
+        for pl in ((0, 1) if plane is None else (plane,)):
+            _check(lib().iqo_hip_plan_set_option(lib().iqo_hip_yuv_plane(self._plan, pl), key.encode(), int(value)),
+                   "set_option")
+
+    def resize(self, srcStY, srcY, srcStUV, srcU, srcV, dstStY, dstY, dstStUV, dstU, dstV):
+        """Host pointers, synchronous."""
+        _check(lib().iqo_hip_resize_yuv420(self._plan, srcStY, _ptr(srcY), srcStUV, _ptr(srcU), _ptr(srcV), dstStY,
+                                           _ptr(dstY), dstStUV, _ptr(dstU), _ptr(dstV)), "resize_yuv420")
+
+    def resize_device(self, nFrames, srcStY, srcStUV, srcFrameSt, srcY, srcU, srcV, dstStY, dstStUV, dstFrameSt,
+                      dstY, dstU, dstV, stream=None):
+        """Device-resident batch (async on `stream`); returns True when one launch did all planes."""
+        fused = ctypes.c_int(0)
+        _check(lib().iqo_hip_resize_yuv420_device(self._plan, nFrames, srcStY, srcStUV, srcFrameSt, _ptr(srcY),
+                                                  _ptr(srcU), _ptr(srcV), dstStY, dstStUV, dstFrameSt, _ptr(dstY),
+                                                  _ptr(dstU), _ptr(dstV), _stream_ptr(stream), ctypes.byref(fused)),
+               "resize_yuv420_device")
+        return bool(fused.value)
+
+    def resize_frames(self, src, out=None, stream=None):
+        """src: uint8 CUDA tensor [frames, srcH*3/2 * srcW] per frame laid out I420 (Y, then U, then V,
+        tightly packed); returns / fills out [frames, dstH*3/2 * dstW].  Returns (out, fused)."""
+        import torch
+        sw, sh, dw, dh = self.srcW, self.srcH, self.dstW, self.dstH
+        cs, cd = (sw // 2) * (sh // 2), (dw // 2) * (dh // 2)
+        n = src.shape[0]
+        if out is None:
+            out = torch.empty((n, dw * dh + 2 * cd), dtype=torch.uint8, device=src.device)
+        b, o = src.data_ptr(), out.data_ptr()
+        fused = self.resize_device(n, sw, sw // 2, src.stride(0), b, b + sw * sh, b + sw * sh + cs,
+                                   dw, dw // 2, out.stride(0), o, o + dw * dh, o + dw * dh + cd, stream)
+        return out, fused

@@ -307,6 +307,139 @@ bool aligned(const void *p, size_t a, size_t st, size_t fst)
     return (reinterpret_cast<uintptr_t>(p) % a) == 0 && (st % a) == 0 && (fst % a) == 0;
 }
 
+// Device-side views of a plan for each kernel family (kernel arguments, no device memory).
+iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
+{
+    const Plan &p = h->p;
+    iqo_amd::LanczosDev l{};
+    const iqo_amd::FastLanczos &f = p.flz;
+    l.KY = f.KY;
+    l.KX = f.KX;
+    l.NY = f.NY;
+    l.NXP = f.NXP;
+    l.offX = f.offX;
+    l.srcW = p.srcW;
+    l.srcH = p.srcH;
+    l.dstW = p.dstW;
+    l.dstH = p.dstH;
+    l.offY = f.offY;
+    for (int i = 0; i < f.NY; ++i)
+        l.cy[i] = pair16(f.cy[i], f.cy[i]);
+    for (int i = 0; i < f.NXP / 2; ++i)
+        l.cx[i] = pair16(f.cx[2 * i], f.cx[2 * i + 1]);
+    l.mainBeginY = f.mainBeginY;
+    l.mainEndY = f.mainEndY;
+    l.mainBeginX = f.mainBeginX;
+    l.mainEndX = f.mainEndX;
+    for (int i = 0; i < 16; ++i) {
+        l.yTopM[i] = f.yTopM[i];
+        l.yTopS[i] = f.yTopS[i];
+        l.yBotM[i] = f.yBotM[i];
+        l.yBotS[i] = f.yBotS[i];
+    }
+    for (int k = 0; k < 8; ++k) {
+        l.xM[k] = f.xM[k];
+        l.xT[k] = f.xT[k];
+    }
+    l.yTopNeg = f.yTopNeg;
+    l.yBotNeg = f.yBotNeg;
+    l.xNeg = f.xNeg;
+    l.dbg = h->debugFlags;
+    l.prefetch = h->prefetch;
+    l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant == 2 ? 2 : 1);
+    l.NX = f.NX;
+    l.offXO = f.offXO;
+    for (int i = 0; i < f.NX / 2 && i < 8; ++i)
+        l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
+    l.np = h->lanes;
+    return l;
+}
+
+iqo_amd::AreaDev area_dev(const iqo_hip_plan *h)
+{
+    const Plan &p = h->p;
+    iqo_amd::AreaDev a{};
+    a.KY = p.far.KY;
+    a.KX = p.far.KX;
+    a.srcW = p.srcW;
+    a.dstW = p.dstW;
+    for (int i = 0; i < a.KY; ++i)
+        a.cy[i] = pair16(p.far.cy[i], p.far.cy[i]);
+    for (int i = 0; i < a.KX / 2; ++i)
+        a.cx[i] = pair16(p.far.cx[2 * i], p.far.cx[2 * i + 1]);
+    a.dstH = p.dstH;
+    return a;
+}
+
+iqo_amd::LinearDev linear_dev(const iqo_hip_plan *h)
+{
+    const Plan &p = h->p;
+    iqo_amd::LinearDev l{};
+    l.srcW = p.srcW;
+    l.srcH = p.srcH;
+    l.dstW = p.dstW;
+    l.dstH = p.dstH;
+    for (int q = 0; q < 2; ++q) {
+        l.cx[q] = pair16(p.fln.cx[q][0], p.fln.cx[q][1]);
+        l.cy[q] = pair16(p.fln.cy[q][0], p.fln.cy[q][1]);
+    }
+    l.dbg = h->debugFlags;
+    l.prefetch = h->linPrefetch;
+    return l;
+}
+
+iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
+{
+    const Plan &p = h->p;
+    iqo_amd::GeneralDev g{};
+    g.method = p.method;
+    g.srcW = p.srcW;
+    g.srcH = p.srcH;
+    g.dstW = p.dstW;
+    g.nX = p.x.taps;
+    g.nY = p.y.taps;
+    g.xInfo = h->dX;
+    g.yInfo = h->dY;
+    g.tabX = h->dTabX;
+    g.tabY = h->dTabY;
+    g.chunks = h->dChunks;
+    g.nChunks = h->nChunks;
+    g.ldsInts = h->ldsInts;
+    return g;
+}
+
+// The kernel family a call with these pointers and strides runs: the plan's fast kernel when the
+// layout has the alignment that kernel's vector accesses need, else the general kernel.
+int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size_t srcFrameSt, const void *dst,
+                      size_t dstSt, size_t dstFrameSt)
+{
+    const Plan &p = h->p;
+    int kernel = h->forceGeneral ? IQO_KERNEL_GENERAL : p.kernel;
+    if (kernel == IQO_KERNEL_LANCZOS_STREAM && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.flz.KX, dstSt, dstFrameSt)))
+        kernel = IQO_KERNEL_GENERAL;
+    if (kernel == IQO_KERNEL_AREA_INT && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.far.KX, dstSt, dstFrameSt)))
+        kernel = IQO_KERNEL_GENERAL;
+    if (kernel == IQO_KERNEL_LINEAR_UP2 && !(aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 16, dstSt, dstFrameSt)))
+        kernel = IQO_KERNEL_GENERAL;
+    return kernel;
+}
+
+iqo_amd::Io make_io(size_t frames, const uint8_t *src, size_t srcSt, size_t srcFrameSt, size_t srcRow0, uint8_t *dst,
+                    size_t dstSt, size_t dstFrameSt, int dstRow0)
+{
+    iqo_amd::Io io;
+    io.frames = static_cast<int>(frames);
+    io.src = src;
+    io.srcSt = static_cast<int64_t>(srcSt);
+    io.srcFrameSt = static_cast<int64_t>(srcFrameSt);
+    io.srcRow0 = static_cast<int>(srcRow0);
+    io.dst = dst;
+    io.dstSt = static_cast<int64_t>(dstSt);
+    io.dstFrameSt = static_cast<int64_t>(dstFrameSt);
+    io.dstRow0 = dstRow0;
+    return io;
+}
+
 int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t srcRow0, size_t srcSt,
              size_t srcFrameSt, const uint8_t *src, size_t dstSt, size_t dstFrameSt, uint8_t *dst, hipStream_t s)
 {
@@ -321,13 +454,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
     if (!guard.ok())
         return IQO_HIP_ENODEV;
 
-    int kernel = h->forceGeneral ? IQO_KERNEL_GENERAL : p.kernel;
-    if (kernel == IQO_KERNEL_LANCZOS_STREAM && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.flz.KX, dstSt, dstFrameSt)))
-        kernel = IQO_KERNEL_GENERAL;
-    if (kernel == IQO_KERNEL_AREA_INT && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.far.KX, dstSt, dstFrameSt)))
-        kernel = IQO_KERNEL_GENERAL;
-    if (kernel == IQO_KERNEL_LINEAR_UP2 && !(aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 16, dstSt, dstFrameSt)))
-        kernel = IQO_KERNEL_GENERAL;
+    const int kernel = kernel_for_layout(h, src, srcSt, srcFrameSt, dst, dstSt, dstFrameSt);
 
     const int rb = static_cast<int>(r0), re = static_cast<int>(r0 + rows);
     // Frames per launch: at most 65535 (grid y), and for the fast kernels at most ~chunkBytes of
@@ -344,101 +471,17 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
         chunk = (nFrames + n - 1) / n;
     }
     for (size_t f0 = 0; f0 < nFrames; f0 += chunk) {
-        iqo_amd::Io io;
-        io.frames = static_cast<int>(std::min(chunk, nFrames - f0));
-        io.src = src + f0 * srcFrameSt;
-        io.srcSt = static_cast<int64_t>(srcSt);
-        io.srcFrameSt = static_cast<int64_t>(srcFrameSt);
-        io.srcRow0 = static_cast<int>(srcRow0);
-        io.dst = dst + f0 * dstFrameSt;
-        io.dstSt = static_cast<int64_t>(dstSt);
-        io.dstFrameSt = static_cast<int64_t>(dstFrameSt);
-        io.dstRow0 = rb;
+        const iqo_amd::Io io = make_io(std::min(chunk, nFrames - f0), src + f0 * srcFrameSt, srcSt, srcFrameSt, srcRow0,
+                                       dst + f0 * dstFrameSt, dstSt, dstFrameSt, rb);
         hipError_t e = hipSuccess;
-        if (kernel == IQO_KERNEL_LANCZOS_STREAM) {
-            iqo_amd::LanczosDev l{};
-            const iqo_amd::FastLanczos &f = p.flz;
-            l.KY = f.KY;
-            l.KX = f.KX;
-            l.NY = f.NY;
-            l.NXP = f.NXP;
-            l.offX = f.offX;
-            l.srcW = p.srcW;
-            l.srcH = p.srcH;
-            l.dstW = p.dstW;
-            l.dstH = p.dstH;
-            l.offY = f.offY;
-            for (int i = 0; i < f.NY; ++i)
-                l.cy[i] = pair16(f.cy[i], f.cy[i]);
-            for (int i = 0; i < f.NXP / 2; ++i)
-                l.cx[i] = pair16(f.cx[2 * i], f.cx[2 * i + 1]);
-            l.mainBeginY = f.mainBeginY;
-            l.mainEndY = f.mainEndY;
-            l.mainBeginX = f.mainBeginX;
-            l.mainEndX = f.mainEndX;
-            for (int i = 0; i < 16; ++i) {
-                l.yTopM[i] = f.yTopM[i];
-                l.yTopS[i] = f.yTopS[i];
-                l.yBotM[i] = f.yBotM[i];
-                l.yBotS[i] = f.yBotS[i];
-            }
-            for (int k = 0; k < 8; ++k) {
-                l.xM[k] = f.xM[k];
-                l.xT[k] = f.xT[k];
-            }
-            l.yTopNeg = f.yTopNeg;
-            l.yBotNeg = f.yBotNeg;
-            l.xNeg = f.xNeg;
-            l.dbg = h->debugFlags;
-            l.prefetch = h->prefetch;
-            l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant == 2 ? 2 : 1);
-            l.NX = f.NX;
-            l.offXO = f.offXO;
-            for (int i = 0; i < f.NX / 2 && i < 8; ++i)
-                l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
-            l.np = h->lanes;
-            e = iqo_amd::launch_lanczos_stream(l, io, rb, re, h->bands, s);
-        } else if (kernel == IQO_KERNEL_AREA_INT) {
-            iqo_amd::AreaDev a{};
-            a.KY = p.far.KY;
-            a.KX = p.far.KX;
-            a.srcW = p.srcW;
-            a.dstW = p.dstW;
-            for (int i = 0; i < a.KY; ++i)
-                a.cy[i] = pair16(p.far.cy[i], p.far.cy[i]);
-            for (int i = 0; i < a.KX / 2; ++i)
-                a.cx[i] = pair16(p.far.cx[2 * i], p.far.cx[2 * i + 1]);
-            e = iqo_amd::launch_area_int(a, io, rb, re, s);
-        } else if (kernel == IQO_KERNEL_LINEAR_UP2) {
-            iqo_amd::LinearDev l{};
-            l.srcW = p.srcW;
-            l.srcH = p.srcH;
-            l.dstW = p.dstW;
-            l.dstH = p.dstH;
-            for (int q = 0; q < 2; ++q) {
-                l.cx[q] = pair16(p.fln.cx[q][0], p.fln.cx[q][1]);
-                l.cy[q] = pair16(p.fln.cy[q][0], p.fln.cy[q][1]);
-            }
-            l.dbg = h->debugFlags;
-            l.prefetch = h->linPrefetch;
-            e = iqo_amd::launch_linear_up2(l, io, rb, re, h->bands, s);
-        } else {
-            iqo_amd::GeneralDev g{};
-            g.method = p.method;
-            g.srcW = p.srcW;
-            g.srcH = p.srcH;
-            g.dstW = p.dstW;
-            g.nX = p.x.taps;
-            g.nY = p.y.taps;
-            g.xInfo = h->dX;
-            g.yInfo = h->dY;
-            g.tabX = h->dTabX;
-            g.tabY = h->dTabY;
-            g.chunks = h->dChunks;
-            g.nChunks = h->nChunks;
-            g.ldsInts = h->ldsInts;
-            e = iqo_amd::launch_general(g, io, rb, re, s);
-        }
+        if (kernel == IQO_KERNEL_LANCZOS_STREAM)
+            e = iqo_amd::launch_lanczos_stream(lanczos_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_AREA_INT)
+            e = iqo_amd::launch_area_int(area_dev(h), io, rb, re, s);
+        else if (kernel == IQO_KERNEL_LINEAR_UP2)
+            e = iqo_amd::launch_linear_up2(linear_dev(h), io, rb, re, h->bands, s);
+        else
+            e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
             return IQO_HIP_EHIP;
     }
@@ -679,6 +722,139 @@ int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dst
         (void)hipStreamSynchronize(st->sOut);
     }
     release_stage(st);
+    return rc;
+}
+
+// ---- YUV 4:2:0 (I420): the reference benchmark's three-plane workload (benchmark.cpp:131-229)
+
+struct iqo_hip_yuv_plan {
+    iqo_hip_plan *y = nullptr, *c = nullptr;  // luma plan, chroma plan (shared by U and V)
+};
+
+int iqo_hip_plan_yuv420(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH, int device,
+                        iqo_hip_yuv_plan **out)
+{
+    if (!out)
+        return IQO_HIP_EINVAL;
+    *out = nullptr;
+    if (srcW < 2 || srcH < 2 || dstW < 2 || dstH < 2)
+        return IQO_HIP_EINVAL;
+    iqo_hip_yuv_plan *yp = new (std::nothrow) iqo_hip_yuv_plan();
+    if (!yp)
+        return IQO_HIP_ENOMEM;
+    int rc = IQO_HIP_EINVAL;
+    if (method == IQO_METHOD_LANCZOS) {
+        // chroma: pxScale 2 (benchmark.cpp:222, sample/resize_yuv420p.cpp:159)
+        rc = iqo_hip_plan_lanczos(degree, srcW, srcH, dstW, dstH, 1, device, &yp->y);
+        if (!rc)
+            rc = iqo_hip_plan_lanczos(degree, srcW / 2, srcH / 2, dstW / 2, dstH / 2, 2, device, &yp->c);
+    } else if (method == IQO_METHOD_AREA) {
+        rc = iqo_hip_plan_area(srcW, srcH, dstW, dstH, device, &yp->y);
+        if (!rc)
+            rc = iqo_hip_plan_area(srcW / 2, srcH / 2, dstW / 2, dstH / 2, device, &yp->c);
+    } else if (method == IQO_METHOD_LINEAR) {
+        rc = iqo_hip_plan_linear(srcW, srcH, dstW, dstH, device, &yp->y);
+        if (!rc)
+            rc = iqo_hip_plan_linear(srcW / 2, srcH / 2, dstW / 2, dstH / 2, device, &yp->c);
+    }
+    if (rc) {
+        iqo_hip_yuv_plan_destroy(yp);
+        return rc;
+    }
+    *out = yp;
+    return IQO_HIP_OK;
+}
+
+void iqo_hip_yuv_plan_destroy(iqo_hip_yuv_plan *yp)
+{
+    if (!yp)
+        return;
+    iqo_hip_plan_destroy(yp->y);
+    iqo_hip_plan_destroy(yp->c);
+    delete yp;
+}
+
+iqo_hip_plan *iqo_hip_yuv_plane(iqo_hip_yuv_plan *yp, int plane)
+{
+    if (!yp)
+        return nullptr;
+    return plane == 0 ? yp->y : plane == 1 ? yp->c : nullptr;
+}
+
+int iqo_hip_resize_yuv420_device(iqo_hip_yuv_plan *yp, size_t nFrames, size_t srcStY, size_t srcStUV,
+                                 size_t srcFrameSt, const uint8_t *srcY, const uint8_t *srcU, const uint8_t *srcV,
+                                 size_t dstStY, size_t dstStUV, size_t dstFrameSt, uint8_t *dstY, uint8_t *dstU,
+                                 uint8_t *dstV, void *stream, int *fused)
+{
+    if (fused)
+        *fused = 0;
+    if (!yp || !yp->y || !yp->c || !srcY || !srcU || !srcV || !dstY || !dstU || !dstV)
+        return IQO_HIP_EINVAL;
+    iqo_hip_plan *hy = yp->y, *hc = yp->c;
+    const Plan &py = hy->p, &pc = hc->p;
+    if (srcStY < static_cast<size_t>(py.srcW) || dstStY < static_cast<size_t>(py.dstW) ||
+        srcStUV < static_cast<size_t>(pc.srcW) || dstStUV < static_cast<size_t>(pc.dstW))
+        return IQO_HIP_EINVAL;
+    if (nFrames == 0)
+        return IQO_HIP_OK;
+    DeviceGuard guard(hy->device);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int ky = kernel_for_layout(hy, srcY, srcStY, srcFrameSt, dstY, dstStY, dstFrameSt);
+    const int ku = kernel_for_layout(hc, srcU, srcStUV, srcFrameSt, dstU, dstStUV, dstFrameSt);
+    const int kv = kernel_for_layout(hc, srcV, srcStUV, srcFrameSt, dstV, dstStUV, dstFrameSt);
+    if (ky == ku && ku == kv && ky != IQO_KERNEL_GENERAL) {
+        // frames per launch: as run_band (65535 grid rows; ~kChunkBytes of frames)
+        const size_t perFrame = py.srcH * srcStY + py.dstH * dstStY + 2 * (pc.srcH * srcStUV + pc.dstH * dstStUV);
+        size_t chunk = std::min<size_t>(65535, std::max<size_t>(1, kChunkBytes / std::max<size_t>(perFrame, 1)));
+        const size_t n = (nFrames + chunk - 1) / chunk;
+        chunk = (nFrames + n - 1) / n;
+        hipError_t e = hipSuccess;
+        for (size_t f0 = 0; f0 < nFrames && e == hipSuccess; f0 += chunk) {
+            const size_t nf = std::min(chunk, nFrames - f0), so = f0 * srcFrameSt, dof = f0 * dstFrameSt;
+            const iqo_amd::Io iy = make_io(nf, srcY + so, srcStY, srcFrameSt, 0, dstY + dof, dstStY, dstFrameSt, 0);
+            const iqo_amd::Io iu = make_io(nf, srcU + so, srcStUV, srcFrameSt, 0, dstU + dof, dstStUV, dstFrameSt, 0);
+            const iqo_amd::Io iv = make_io(nf, srcV + so, srcStUV, srcFrameSt, 0, dstV + dof, dstStUV, dstFrameSt, 0);
+            if (ky == IQO_KERNEL_LANCZOS_STREAM)
+                e = iqo_amd::launch_yuv420_lanczos(lanczos_dev(hy), iy, lanczos_dev(hc), iu, iv, s);
+            else if (ky == IQO_KERNEL_AREA_INT)
+                e = iqo_amd::launch_yuv420_area(area_dev(hy), iy, area_dev(hc), iu, iv, s);
+            else
+                e = iqo_amd::launch_yuv420_linear(linear_dev(hy), iy, linear_dev(hc), iu, iv, s);
+        }
+        if (e == hipSuccess) {
+            if (fused)
+                *fused = 1;
+            return IQO_HIP_OK;
+        }
+        if (e != hipErrorNotSupported)
+            return IQO_HIP_EHIP;
+        (void)hipGetLastError();
+    }
+    // plane by plane
+    int rc = run_band(hy, nFrames, 0, static_cast<size_t>(py.dstH), 0, srcStY, srcFrameSt, srcY, dstStY, dstFrameSt,
+                      dstY, s);
+    if (!rc)
+        rc = run_band(hc, nFrames, 0, static_cast<size_t>(pc.dstH), 0, srcStUV, srcFrameSt, srcU, dstStUV, dstFrameSt,
+                      dstU, s);
+    if (!rc)
+        rc = run_band(hc, nFrames, 0, static_cast<size_t>(pc.dstH), 0, srcStUV, srcFrameSt, srcV, dstStUV, dstFrameSt,
+                      dstV, s);
+    return rc;
+}
+
+int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *srcY, size_t srcStUV,
+                          const uint8_t *srcU, const uint8_t *srcV, size_t dstStY, uint8_t *dstY, size_t dstStUV,
+                          uint8_t *dstU, uint8_t *dstV)
+{
+    if (!yp)
+        return IQO_HIP_EINVAL;
+    int rc = iqo_hip_resize(yp->y, srcStY, srcY, dstStY, dstY);
+    if (!rc)
+        rc = iqo_hip_resize(yp->c, srcStUV, srcU, dstStUV, dstU);
+    if (!rc)
+        rc = iqo_hip_resize(yp->c, srcStUV, srcV, dstStUV, dstV);
     return rc;
 }
 

@@ -303,7 +303,7 @@ __device__ __forceinline__ uint32_t ydiv2(uint32_t w, uint32_t m, int s)
 }
 
 template <int KY, int KX, int NY, int NXP, int OFFXD, int PD>
-__global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
+__device__ __forceinline__ void lanczos_stream_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
 {
     constexpr int OUTS = 16 / KX;            // outputs per producing lane
     constexpr int OPW = 62 * OUTS;           // outputs per wave (lanes 1..62)
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
     // rows, the row counter) is treated as divergent -- row offsets land in VGPRs, every buffer
     // load becomes a readfirstlane loop and row branches become exec-mask branches
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const int g = static_cast<int>(blockIdx.x) * 4 + wib;  // wave index in the (band, column) grid
+    const int g = static_cast<int>(bx) * 4 + wib;  // wave index in the (band, column) grid
     if (g >= a.bands * a.wavesPerRow)
         return;  // whole wave: nothing below synchronises across waves
     const int band = g / a.wavesPerRow, wcol = g - band * a.wavesPerRow;
@@ -339,8 +339,8 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
     const bool edgeL = x0 == 0, edgeR = x0 + OPW >= L.dstW;       // wave holds border columns
     const bool laneL = outX == 0, laneR = outX == L.dstW - OUTS;  // ... in this lane
 
-    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
-    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
     const __amdgpu_buffer_rsrc_t srcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
@@ -469,6 +469,12 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
         });
     }
 }
+template <int KY, int KX, int NY, int NXP, int OFFXD, int PD>
+__global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
+{
+    lanczos_stream_kernel_body<KY, KX, NY, NXP, OFFXD, PD>(a, blockIdx.x, blockIdx.y);
+}
+
 
 // ================================================================ symmetric Lanczos streamer
 //
@@ -536,7 +542,7 @@ __device__ __forceinline__ void wait_vmcnt()
 #endif
 
 template <int NY, int NX, int OFFX, int K, bool C0ONE>
-__global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
+__device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
 {
     constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
     static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
@@ -551,7 +557,7 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
     const LanczosDev &L = a.l;
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const int g = static_cast<int>(blockIdx.x) * 4 + wib;
+    const int g = static_cast<int>(bx) * 4 + wib;
     if (g >= a.bands * a.wavesPerRow)
         return;
     const int band = g / a.wavesPerRow, wcol = g - band * a.wavesPerRow;
@@ -569,8 +575,8 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
     const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
     const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
 
-    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
-    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
     const __amdgpu_buffer_rsrc_t srcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
@@ -761,6 +767,12 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
+template <int NY, int NX, int OFFX, int K, bool C0ONE>
+__global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
+{
+    lanczos_sym_kernel_body<NY, NX, OFFX, K, C0ONE>(a, blockIdx.x, blockIdx.y);
+}
+
 
 // ================================================================ block-shared symmetric streamer
 //
@@ -782,8 +794,7 @@ template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
 #ifndef IQO_SYMB_EDGE_BATCH
 #define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (C2: 64 -> 16 cuts write traffic +4.5% -> +2%)
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WAVES_PER_EU))) void
-lanczos_symb_kernel(LanczosArgs a)
+__device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
 {
     constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
     static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
@@ -803,7 +814,7 @@ lanczos_symb_kernel(LanczosArgs a)
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const int wpr = a.wavesPerRow;                 // = waves of this workgroup
-    const int band = static_cast<int>(blockIdx.x), wcol = wib;
+    const int band = static_cast<int>(bx), wcol = wib;
     const int y0 = a.rowBegin + band * a.rowsPerBand;
     const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
     if (y0 >= y1)
@@ -819,8 +830,8 @@ lanczos_symb_kernel(LanczosArgs a)
     const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
     const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
 
-    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
-    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
     const __amdgpu_buffer_rsrc_t srcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
@@ -1027,6 +1038,12 @@ lanczos_symb_kernel(LanczosArgs a)
 
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WAVES_PER_EU))) void lanczos_symb_kernel(LanczosArgs a)
+{
+    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, blockIdx.x, blockIdx.y);
+}
+
 
 // ================================================================ Area integer ratio
 //
@@ -1040,17 +1057,17 @@ struct AreaArgs {
 };
 
 template <int KX, int KYT>
-__global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
+__device__ __forceinline__ void area_int_kernel_body(const AreaArgs &a, const unsigned bx, const unsigned by)
 {
     constexpr int OUTS = 16 / KX;
     const int KY = KYT ? KYT : a.g.KY;
-    const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t gid = static_cast<int64_t>(bx) * blockDim.x + threadIdx.x;
     const int64_t total = static_cast<int64_t>(a.rowEnd - a.rowBegin) * a.groups;
     if (gid >= total)
         return;
     const int y = a.rowBegin + static_cast<int>(gid / a.groups);
     const int gcol = static_cast<int>(gid % a.groups);
-    const uint8_t *s = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt +
+    const uint8_t *s = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt +
                        static_cast<int64_t>(KY * y - a.io.srcRow0) * a.io.srcSt + 16 * gcol;
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll 4
@@ -1073,7 +1090,7 @@ __global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
         uint16_t u = static_cast<uint16_t>(v);
         out[k] = opaque(u > 255 ? 255u : u);
     }
-    uint8_t *d = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt +
+    uint8_t *d = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt +
                  static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt + OUTS * gcol;
     if constexpr (OUTS == 8) {
         *reinterpret_cast<uint2 *>(d) = make_uint2(out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24),
@@ -1086,6 +1103,12 @@ __global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
         d[0] = static_cast<uint8_t>(out[0]);
     }
 }
+template <int KX, int KYT>
+__global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
+{
+    area_int_kernel_body<KX, KYT>(a, blockIdx.x, blockIdx.y);
+}
+
 
 // ================================================================ exact 2x bilinear streamer
 //
@@ -1132,13 +1155,13 @@ __device__ __forceinline__ uint32_t pack23_hi(uint32_t w, uint32_t a, uint32_t b
 }
 
 template <int PD, bool NTST>
-__global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
+__device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, const unsigned bx, const unsigned by)
 {
     static_assert(PD % 2 == 0, "the unroll must also cover the 2-slot row ring");
     const LinearDev &g = a.g;
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const int gw = static_cast<int>(blockIdx.x) * 4 + wib;
+    const int gw = static_cast<int>(bx) * 4 + wib;
     if (gw >= a.bands * a.wavesPerRow)
         return;
     const int band = gw / a.wavesPerRow, wcol = gw - band * a.wavesPerRow;
@@ -1157,8 +1180,8 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
     const uint32_t cxFirst = cb == 0 ? 0x80000000u : g.cx[0];
     const uint32_t cxLast = cb + 8 == g.srcW ? 0x00008000u : g.cx[1];
 
-    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.y) * a.io.srcFrameSt;
-    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.y) * a.io.dstFrameSt;
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
     const __amdgpu_buffer_rsrc_t srcR =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
@@ -1262,6 +1285,85 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
     if (y1 == g.dstH && g.dstH > 1)
         border_row(g.dstH - 1, g.srcH - 1);
 }
+template <int PD, bool NTST>
+__global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
+{
+    linear_up2_kernel_body<PD, NTST>(a, blockIdx.x, blockIdx.y);
+}
+
+
+// ================================================================ YUV 4:2:0 in one launch
+//
+// The three planes of a batch of I420 frames (the reference benchmark's workload,
+// benchmark.cpp:206-229: Y at full size, U and V at half size, Lanczos chroma with pxScale 2) in
+// ONE launch: grid.z = plane, grid.x covers the larger plane grid, blocks past a plane's own grid
+// exit.  The plane bodies are the single-plane kernels' bodies; Y and chroma may use different
+// kernels (e.g. block-shared symmetric Y + accumulator-ring chroma).  All bodies use 256-thread
+// blocks here (the block-shared Y body only when its row takes exactly 4 waves).
+
+template <typename AY, typename AC>
+struct Yuv3Args {
+    AY y;
+    AC u, v;
+    unsigned gxY, gxC;  // grid.x of the Y plane / of each chroma plane
+};
+
+template <int NY, int NX, int OFFX, bool ONE>
+struct SymbY {
+    static __device__ __forceinline__ void run(const LanczosArgs &a, unsigned bx, unsigned by)
+    {
+        lanczos_symb_kernel_body<NY, NX, OFFX, 4, 1, ONE>(a, bx, by);
+    }
+};
+template <int NY, int NX, int OFFX, bool ONE>
+struct SymY {
+    static __device__ __forceinline__ void run(const LanczosArgs &a, unsigned bx, unsigned by)
+    {
+        lanczos_sym_kernel_body<NY, NX, OFFX, 4, ONE>(a, bx, by);
+    }
+};
+struct RingChroma {  // pxScale-2 chroma tables of Lanczos-2/3 2:1 (3 taps padded to 4)
+    static __device__ __forceinline__ void run(const LanczosArgs &a, unsigned bx, unsigned by)
+    {
+        lanczos_stream_kernel_body<2, 2, 4, 4, 0, 3>(a, bx, by);
+    }
+};
+template <int KX, int KYT>
+struct AreaPlane {
+    static __device__ __forceinline__ void run(const AreaArgs &a, unsigned bx, unsigned by)
+    {
+        area_int_kernel_body<KX, KYT>(a, bx, by);
+    }
+};
+struct LinearPlane {
+    static __device__ __forceinline__ void run(const LinearArgs &a, unsigned bx, unsigned by)
+    {
+        linear_up2_kernel_body<2, true>(a, bx, by);
+    }
+};
+
+template <typename BY, typename BC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void
+yuv420_lanczos_kernel(Yuv3Args<LanczosArgs, LanczosArgs> a)
+{
+    if (blockIdx.z == 0) {
+        if (blockIdx.x < a.gxY)
+            BY::run(a.y, blockIdx.x, blockIdx.y);
+    } else if (blockIdx.x < a.gxC) {
+        BC::run(blockIdx.z == 1 ? a.u : a.v, blockIdx.x, blockIdx.y);
+    }
+}
+
+template <typename B, typename A>
+__global__ __launch_bounds__(256) void yuv420_plane_kernel(Yuv3Args<A, A> a)
+{
+    if (blockIdx.z == 0) {
+        if (blockIdx.x < a.gxY)
+            B::run(a.y, blockIdx.x, blockIdx.y);
+    } else if (blockIdx.x < a.gxC) {
+        B::run(blockIdx.z == 1 ? a.u : a.v, blockIdx.x, blockIdx.y);
+    }
+}
 
 } // namespace
 
@@ -1344,11 +1446,19 @@ bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)
 
 int lanczos_stream_block(int) { return 256; }
 
-hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
-                                 hipStream_t s)
+// One prepared launch of a band-walking kernel: arguments, geometry and the instantiation.
+template <typename A>
+struct Prep {
+    A a;
+    dim3 grid;
+    int block = 256, lds = 0;
+    const void *kern = nullptr;
+    int kind = 0;  // Lanczos: 0 accumulator ring, 1 block-shared symmetric, 2 per-wave symmetric
+    int pd = 0;    // prefetch / ring depth the instantiation was chosen for
+};
+
+hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands, Prep<LanczosArgs> *P)
 {
-    if (rowEnd <= rowBegin || io.frames <= 0)
-        return hipSuccess;
     const int rows = rowEnd - rowBegin;
     int opw = 62 * (16 / l.KX);
     int wpr = (l.dstW + opw - 1) / opw;
@@ -1417,7 +1527,8 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     bands = max(1, min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
-    LanczosArgs a{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks};
+    LanczosArgs &a = P->a;
+    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks};
     // buffer ranges: the source window spans rows [srcRow0, srcH) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(l.srcH - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -1428,37 +1539,55 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
-    const dim3 grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
-                             : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
-    void *args[] = {&a};
-    return hipLaunchKernel(kern, grid, dim3(static_cast<unsigned>(block)), args, static_cast<size_t>(ldsBytes), s);
+    P->grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
+                     : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    P->block = block;
+    P->lds = ldsBytes;
+    P->kern = kern;
+    P->kind = shared ? 1 : (l.sym ? 2 : 0);
+    P->pd = pd;
+    return hipSuccess;
+}
+
+hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
+                                 hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    Prep<LanczosArgs> P;
+    hipError_t e = prep_lanczos(l, io, rowBegin, rowEnd, bands, &P);
+    if (e != hipSuccess)
+        return e;
+    void *args[] = {&P.a};
+    return hipLaunchKernel(P.kern, P.grid, dim3(static_cast<unsigned>(P.block)), args, static_cast<size_t>(P.lds), s);
+}
+
+hipError_t prep_area(const AreaDev &g, const Io &io, int rowBegin, int rowEnd, Prep<AreaArgs> *P)
+{
+    P->a = AreaArgs{g, io, rowBegin, rowEnd, g.srcW / 16};
+    const int64_t total = static_cast<int64_t>(rowEnd - rowBegin) * P->a.groups;
+    P->grid = dim3(static_cast<unsigned>((total + 255) / 256), static_cast<unsigned>(io.frames));
+    P->kind = g.KX == 4 && g.KY == 4 ? 0 : g.KX == 2 && g.KY == 2 ? 1 : g.KX == 2 ? 2 : g.KX == 4 ? 3 : 4;
+    static const void *const kerns[5] = {
+        reinterpret_cast<const void *>(area_int_kernel<4, 4>), reinterpret_cast<const void *>(area_int_kernel<2, 2>),
+        reinterpret_cast<const void *>(area_int_kernel<2, 0>), reinterpret_cast<const void *>(area_int_kernel<4, 0>),
+        reinterpret_cast<const void *>(area_int_kernel<8, 0>)};
+    P->kern = kerns[P->kind];
+    return hipSuccess;
 }
 
 hipError_t launch_area_int(const AreaDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    AreaArgs a{g, io, rowBegin, rowEnd, g.srcW / 16};
-    int64_t total = static_cast<int64_t>(rowEnd - rowBegin) * a.groups;
-    dim3 grid(static_cast<unsigned>((total + 255) / 256), static_cast<unsigned>(io.frames));
-    if (g.KX == 4 && g.KY == 4)
-        hipLaunchKernelGGL((area_int_kernel<4, 4>), grid, dim3(256), 0, s, a);
-    else if (g.KX == 2 && g.KY == 2)
-        hipLaunchKernelGGL((area_int_kernel<2, 2>), grid, dim3(256), 0, s, a);
-    else if (g.KX == 2)
-        hipLaunchKernelGGL((area_int_kernel<2, 0>), grid, dim3(256), 0, s, a);
-    else if (g.KX == 4)
-        hipLaunchKernelGGL((area_int_kernel<4, 0>), grid, dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL((area_int_kernel<8, 0>), grid, dim3(256), 0, s, a);
-    return hipGetLastError();
+    Prep<AreaArgs> P;
+    (void)prep_area(g, io, rowBegin, rowEnd, &P);
+    void *args[] = {&P.a};
+    return hipLaunchKernel(P.kern, P.grid, dim3(256), args, 0, s);
 }
 
-hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, int bands,
-                             hipStream_t s)
+hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, int bands, Prep<LinearArgs> *P)
 {
-    if (rowEnd <= rowBegin || io.frames <= 0)
-        return hipSuccess;
     if (g.srcW % 8 || g.dstW != 2 * g.srcW || g.srcW < 8)
         return hipErrorInvalidValue;
     const int rows = rowEnd - rowBegin;
@@ -1482,7 +1611,8 @@ hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int
     bands = max(1, min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
-    LinearArgs a{g, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, np};
+    LinearArgs &a = P->a;
+    a = LinearArgs{g, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, np};
     const int64_t sb = static_cast<int64_t>(g.srcH - io.srcRow0 - 1) * io.srcSt + g.srcW;
     const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + g.dstW;
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31))
@@ -1490,9 +1620,118 @@ hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
-    dim3 grid(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    P->grid = dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    P->kern = kern;
+    P->kind = nt ? 1 : 0;
+    P->pd = pd;
+    return hipSuccess;
+}
+
+hipError_t launch_linear_up2(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, int bands,
+                             hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    Prep<LinearArgs> P;
+    hipError_t e = prep_linear(g, io, rowBegin, rowEnd, bands, &P);
+    if (e != hipSuccess)
+        return e;
+    void *args[] = {&P.a};
+    return hipLaunchKernel(P.kern, P.grid, dim3(256), args, 0, s);
+}
+
+
+// ---- YUV 4:2:0 launchers: one launch for the three planes when the planes' kernels have a fused
+// instantiation, else hipErrorNotSupported (the caller then launches plane by plane).
+
+template <typename A>
+hipError_t launch_fused3(const void *kern, const Prep<A> &y, const Prep<A> &u, const Prep<A> &v, int block, int lds,
+                         hipStream_t s)
+{
+    Yuv3Args<A, A> a{y.a, u.a, v.a, y.grid.x, u.grid.x};
+    const dim3 grid(std::max(y.grid.x, u.grid.x), y.grid.y, 3);
     void *args[] = {&a};
-    return hipLaunchKernel(kern, grid, dim3(256), args, 0, s);
+    return hipLaunchKernel(kern, grid, dim3(static_cast<unsigned>(block)), args, static_cast<size_t>(lds), s);
+}
+
+hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const LanczosDev &lc, const Io &ioU,
+                                 const Io &ioV, hipStream_t s)
+{
+    if (ioY.frames <= 0)
+        return hipSuccess;
+    if (ioY.frames != ioU.frames || ioU.frames != ioV.frames)
+        return hipErrorInvalidValue;
+    Prep<LanczosArgs> py, pu, pv;
+    hipError_t e;
+    if ((e = prep_lanczos(ly, ioY, 0, ly.dstH, 0, &py)) != hipSuccess ||
+        (e = prep_lanczos(lc, ioU, 0, lc.dstH, 0, &pu)) != hipSuccess ||
+        (e = prep_lanczos(lc, ioV, 0, lc.dstH, 0, &pv)) != hipSuccess)
+        return e;
+    // chroma: the ring instantiation at the default depth; Y: a symmetric streamer at K = 4 whose
+    // blocks are 256 threads (block-shared only with exactly 4 waves per row)
+    if (pu.kind != 0 || lc.NY != 4 || pu.pd != 3 || py.kind == 0 || py.pd < 3)
+        return hipErrorNotSupported;
+    const bool one = (ly.cy[0] & 0xffffu) == 1u;
+    const bool shared = py.kind == 1 && py.block == 256 && py.a.chunks <= 4;
+    const void *kern = nullptr;
+    if (ly.NY == 10 && one)
+        kern = shared ? reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymbY<10, 12, -5, true>, RingChroma>)
+                      : reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymY<10, 12, -5, true>, RingChroma>);
+    else if (ly.NY == 8)
+        kern = shared ? reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymbY<8, 8, -3, false>, RingChroma>)
+                      : reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymY<8, 8, -3, false>, RingChroma>);
+    else
+        return hipErrorNotSupported;
+    if (!shared && py.kind == 1) {
+        // re-prepare Y as the per-wave symmetric streamer (256-thread blocks of 4 waves)
+        LanczosDev l2 = ly;
+        l2.sym = 2;
+        if ((e = prep_lanczos(l2, ioY, 0, ly.dstH, 0, &py)) != hipSuccess)
+            return e;
+    }
+    // the symmetric Y bodies need their LDS: dynamic for the block-shared body, static otherwise
+    return launch_fused3(kern, py, pu, pv, 256, shared ? py.lds : 0, s);
+}
+
+hipError_t launch_yuv420_area(const AreaDev &gy, const Io &ioY, const AreaDev &gc, const Io &ioU, const Io &ioV,
+                              hipStream_t s)
+{
+    if (ioY.frames <= 0)
+        return hipSuccess;
+    if (ioY.frames != ioU.frames || ioU.frames != ioV.frames)
+        return hipErrorInvalidValue;
+    Prep<AreaArgs> py, pu, pv;
+    (void)prep_area(gy, ioY, 0, gy.dstH, &py);
+    (void)prep_area(gc, ioU, 0, gc.dstH, &pu);
+    (void)prep_area(gc, ioV, 0, gc.dstH, &pv);
+    if (py.kind != pu.kind || (py.kind >= 2 && gy.KY != gc.KY))
+        return hipErrorNotSupported;
+    static const void *const kerns[5] = {
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<4, 4>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<2, 2>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<2, 0>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<4, 0>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<8, 0>, AreaArgs>)};
+    return launch_fused3(kerns[py.kind], py, pu, pv, 256, 0, s);
+}
+
+hipError_t launch_yuv420_linear(const LinearDev &gy, const Io &ioY, const LinearDev &gc, const Io &ioU,
+                                const Io &ioV, hipStream_t s)
+{
+    if (ioY.frames <= 0)
+        return hipSuccess;
+    if (ioY.frames != ioU.frames || ioU.frames != ioV.frames)
+        return hipErrorInvalidValue;
+    Prep<LinearArgs> py, pu, pv;
+    hipError_t e;
+    if ((e = prep_linear(gy, ioY, 0, gy.dstH, 0, &py)) != hipSuccess ||
+        (e = prep_linear(gc, ioU, 0, gc.dstH, 0, &pu)) != hipSuccess ||
+        (e = prep_linear(gc, ioV, 0, gc.dstH, 0, &pv)) != hipSuccess)
+        return e;
+    if (py.kind != 1 || pu.kind != 1 || py.pd != 2 || pu.pd != 2)
+        return hipErrorNotSupported;
+    return launch_fused3(reinterpret_cast<const void *>(yuv420_plane_kernel<LinearPlane, LinearArgs>), py, pu, pv,
+                         256, 0, s);
 }
 
 } // namespace iqo_amd

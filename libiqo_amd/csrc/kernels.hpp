@@ -58,7 +58,7 @@ int lanczos_stream_block(int srcW);
 
 // --- Area integer-ratio kernel.
 struct AreaDev {
-    int KY, KX, srcW, dstW;
+    int KY, KX, srcW, dstW, dstH;
     uint32_t cy[16];             // (c, c) u16 pairs
     uint32_t cx[8];              // (c_2p, c_2p+1) u16 pairs
 };
@@ -74,5 +74,15 @@ struct LinearDev {
 };
 hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
                              hipStream_t s);
+
+// --- YUV 4:2:0: the Y, U and V planes of a batch in ONE launch (grid.z = plane) when both plane
+// kinds have a fused instantiation; hipErrorNotSupported otherwise (launch plane by plane).
+// Frame f of each plane: Io as above; all three Io must hold the same frame count.
+hipError_t launch_yuv420_lanczos(const LanczosDev &y, const Io &ioY, const LanczosDev &c, const Io &ioU,
+                                 const Io &ioV, hipStream_t s);
+hipError_t launch_yuv420_area(const AreaDev &y, const Io &ioY, const AreaDev &c, const Io &ioU, const Io &ioV,
+                              hipStream_t s);
+hipError_t launch_yuv420_linear(const LinearDev &y, const Io &ioY, const LinearDev &c, const Io &ioU,
+                                const Io &ioV, hipStream_t s);
 
 } // namespace iqo_amd

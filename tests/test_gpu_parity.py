@@ -274,6 +274,55 @@ def test_host_pointer_pipeline_pinned_and_pageable(cfg):
     assert (got[:, dw:] == 7).all(), "bytes past the row written"
 
 
+YUV_CASES = [
+    ("lanczos", 3, 3840, 2160, 1920, 1080, True),   # block-shared symmetric Y + ring chroma, one launch
+    ("lanczos", 2, 640, 480, 320, 240, True),       # per-wave symmetric Y (1 wave per row) + ring chroma
+    ("area", 0, 7680, 4320, 1920, 1080, True),
+    ("linear", 0, 1920, 1080, 3840, 2160, True),
+    ("lanczos", 3, 1920, 1080, 1280, 720, False),   # general kernel: plane by plane
+]
+
+
+@pytest.mark.parametrize("case", YUV_CASES, ids=lambda c: "%s%d_%dx%d" % c[:4])
+def test_yuv420_planes_match_oracle(case):
+    """I420 batch through iqo_hip_resize_yuv420_device: each plane equals the oracle on that plane
+    (Lanczos chroma with pxScale 2, as the reference benchmark builds it, benchmark.cpp:222)."""
+    m, d, sw, sh, dw, dh, want_fused = case
+    n = 2
+    cw, ch, cdw, cdh = sw // 2, sh // 2, dw // 2, dh // 2
+    y = _noise_batch(n, sw, sh, 900)
+    u = _noise_batch(n, cw, ch, 910)
+    v = _noise_batch(n, cw, ch, 920)
+    v[1, : ch // 2] = 255
+    src = torch.from_numpy(np.concatenate([y.reshape(n, -1), u.reshape(n, -1), v.reshape(n, -1)], axis=1)).to(DEV)
+    r = libiqo_amd.Yuv420Resizer(m, d, sw, sh, dw, dh)
+    out, fused = r.resize_frames(src)
+    out = out.cpu().numpy()
+    assert fused == want_fused
+    pxc = 2 if m == "lanczos" else 1
+    for f in range(n):
+        oy = out[f, : dw * dh].reshape(dh, dw)
+        ou = out[f, dw * dh: dw * dh + cdw * cdh].reshape(cdh, cdw)
+        ov = out[f, dw * dh + cdw * cdh:].reshape(cdh, cdw)
+        assert (oy == ol.run_oracle(m, d, sw, sh, dw, dh, 1, y[f])).all(), (case, f, "Y")
+        assert (ou == ol.run_oracle(m, d, cw, ch, cdw, cdh, pxc, u[f])).all(), (case, f, "U")
+        assert (ov == ol.run_oracle(m, d, cw, ch, cdw, cdh, pxc, v[f])).all(), (case, f, "V")
+
+
+def test_yuv420_host_pointers():
+    m, d, sw, sh, dw, dh = "lanczos", 2, 640, 480, 320, 240
+    y = ol.gen("noise", sw, sh, 31)
+    u = ol.gen("noise", sw // 2, sh // 2, 32)
+    v = ol.gen("noise", sw // 2, sh // 2, 33)
+    oy = np.zeros((dh, dw), np.uint8)
+    ou = np.zeros((dh // 2, dw // 2), np.uint8)
+    ov = np.zeros((dh // 2, dw // 2), np.uint8)
+    libiqo_amd.Yuv420Resizer(m, d, sw, sh, dw, dh).resize(sw, y, sw // 2, u, v, dw, oy, dw // 2, ou, ov)
+    assert (oy == ol.run_oracle(m, d, sw, sh, dw, dh, 1, y)).all()
+    assert (ou == ol.run_oracle(m, d, sw // 2, sh // 2, dw // 2, dh // 2, 2, u)).all()
+    assert (ov == ol.run_oracle(m, d, sw // 2, sh // 2, dw // 2, dh // 2, 2, v)).all()
+
+
 @pytest.mark.parametrize("value", [0, 255])
 def test_flat_frames_stay_flat_full_size(value):
     for m, d, sw, sh, dw, dh, px in CONFIGS[:3]:
