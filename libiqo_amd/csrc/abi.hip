@@ -38,14 +38,13 @@ struct iqo_hip_plan {
     int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
                             // streamer, 2: per-wave symmetric streamer
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
-    int chunkFrames = 0;    // frames per launch (0 = auto: about kChunkBytes of frames)
+    int chunkFrames = 0;    // frames per launch (0 = up to 65535)
 };
 
 namespace {
 
 constexpr int kChunkOut = 256;     // outputs per general-kernel chunk (= workgroup size)
 constexpr int kChunkLds = 8192;    // max work-row ints per chunk (32 KiB LDS)
-constexpr size_t kChunkBytes = size_t(1400) << 20;  // frames per launch of the fast kernels
 
 class DeviceGuard {  // restore the caller's current device
 public:
@@ -457,16 +456,12 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
     const int kernel = kernel_for_layout(h, src, srcSt, srcFrameSt, dst, dstSt, dstFrameSt);
 
     const int rb = static_cast<int>(r0), re = static_cast<int>(r0 + rows);
-    // Frames per launch: at most 65535 (grid y), and for the fast kernels at most ~chunkBytes of
-    // frames (source window + output band): past ~1.3 GB per launch the same kernels lose
-    // 20-25 % of their HBM rate on MI355X (C2 at 160..256 frames per launch), while a launch
-    // boundary costs ~2 us.
+    // Frames per launch: at most 65535 (grid y).  The option "chunk_frames" splits further into
+    // equal launches (measured: no gain on MI355X for C2 at 256 frames, a loss for C3 at 48 --
+    // the per-frame slowdown of C2 past ~130 frames per call is not a per-launch effect).
     size_t chunk = 65535;
-    if (kernel != IQO_KERNEL_GENERAL) {
-        const size_t perFrame = (p.srcH - srcRow0) * srcSt + rows * dstSt;
-        const size_t cap = h->chunkFrames > 0 ? static_cast<size_t>(h->chunkFrames)
-                                              : std::max<size_t>(1, kChunkBytes / std::max<size_t>(perFrame, 1));
-        chunk = std::min(chunk, cap);
+    if (h->chunkFrames > 0) {
+        chunk = std::min(chunk, static_cast<size_t>(h->chunkFrames));
         const size_t n = (nFrames + chunk - 1) / chunk;  // equal launches, not one straggler
         chunk = (nFrames + n - 1) / n;
     }
@@ -805,9 +800,8 @@ int iqo_hip_resize_yuv420_device(iqo_hip_yuv_plan *yp, size_t nFrames, size_t sr
     const int ku = kernel_for_layout(hc, srcU, srcStUV, srcFrameSt, dstU, dstStUV, dstFrameSt);
     const int kv = kernel_for_layout(hc, srcV, srcStUV, srcFrameSt, dstV, dstStUV, dstFrameSt);
     if (ky == ku && ku == kv && ky != IQO_KERNEL_GENERAL) {
-        // frames per launch: as run_band (65535 grid rows; ~kChunkBytes of frames)
-        const size_t perFrame = py.srcH * srcStY + py.dstH * dstStY + 2 * (pc.srcH * srcStUV + pc.dstH * dstStUV);
-        size_t chunk = std::min<size_t>(65535, std::max<size_t>(1, kChunkBytes / std::max<size_t>(perFrame, 1)));
+        // frames per launch: as run_band
+        size_t chunk = std::min<size_t>(65535, hy->chunkFrames > 0 ? static_cast<size_t>(hy->chunkFrames) : 65535);
         const size_t n = (nFrames + chunk - 1) / chunk;
         chunk = (nFrames + n - 1) / n;
         hipError_t e = hipSuccess;

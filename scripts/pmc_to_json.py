@@ -17,7 +17,7 @@ import os
 import statistics
 import sys
 
-KERNELS = {"lanczos_stream": "lanczos_stream_kernel", "area_int": "area_int_kernel",
+KERNELS = {"lanczos_stream": "lanczos_s", "area_int": "area_int_kernel",  # lanczos_s: symb / sym / stream
            "linear_up2": "linear_up2_kernel", "general": "general_kernel"}
 BENCH = {"c2": ("lanczos_stream", 128), "c3": ("area_int", 48), "c4": ("linear_up2", 128), "c1": ("lanczos_stream", 4096)}
 
