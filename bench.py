@@ -32,6 +32,10 @@ CONFIGS = {
     "c3": ("area", 0, 7680, 4320, 1920, 1080, 1, 48, "C3 Area U8 1ch 7680x4320->1920x1080"),
     "c4": ("linear", 0, 1920, 1080, 3840, 2160, 1, 128, "C4 Linear U8 1ch 1920x1080->3840x2160"),
     "c1": ("lanczos", 2, 640, 480, 320, 240, 1, 4096, "C1 Lanczos-2 U8 1ch 640x480->320x240"),
+    # general-kernel shapes (not BASELINE configs): multi-phase downscale, Lanczos upscale
+    "g1": ("lanczos", 3, 1920, 1080, 1280, 720, 1, 128, "G1 Lanczos-3 U8 1ch 1920x1080->1280x720"),
+    "g2": ("lanczos", 3, 1920, 1080, 3840, 2160, 1, 32, "G2 Lanczos-3 U8 1ch 1920x1080->3840x2160"),
+    "g3": ("area", 0, 1920, 1080, 1280, 720, 1, 128, "G3 Area U8 1ch 1920x1080->1280x720"),
 }
 
 

@@ -952,6 +952,9 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         // this wave's DMA(i) retired: after it come the store of iteration i-K+1 and the 2*CPW
         // DMAs + 1 store of each of iterations i-K+2 .. i-1; then the workgroup barrier makes
         // every wave's chunks of iteration i visible and retires all reads of slot (i-1) mod K
+#ifdef IQO_EXP_SETPRIO
+        __builtin_amdgcn_s_setprio(IQO_EXP_SETPRIO);
+#endif
         wait_vmcnt<WAIT>();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -959,6 +962,9 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         uint4 n0, n1;
         read_iter(i, n0, n1);
         dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
+#ifdef IQO_EXP_SETPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
 #ifdef IQO_EXP_MEMONLY  // timing experiment: memory stream only (wrong output)
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{n0.x ^ n1.y, n0.z ^ n1.w}, dstR, stoff, (yy - a.io.dstRow0) * dstSt,
                                               IQO_SYM_STORE_AUX);
