@@ -50,10 +50,11 @@ enum { IQO_METHOD_LANCZOS = 0, IQO_METHOD_AREA = 1, IQO_METHOD_LINEAR = 2 };
 
 /* Kernel families a plan can dispatch to (iqo_hip_plan_desc.kernel). */
 enum {
-    IQO_KERNEL_GENERAL = 0,     /* any shape: one workgroup per output row, LDS work row */
+    IQO_KERNEL_GENERAL = 0,     /* any shape, any layout: one workgroup per output row (reference kernel) */
     IQO_KERNEL_LANCZOS_STREAM = 1, /* integer ratio, 1 phase: row-band walker, register window */
     IQO_KERNEL_AREA_INT = 2,    /* integer ratio area */
-    IQO_KERNEL_LINEAR_UP2 = 3   /* exact 2x bilinear upsampling */
+    IQO_KERNEL_LINEAR_UP2 = 3,  /* exact 2x bilinear upsampling */
+    IQO_KERNEL_TILE = 4         /* any other shape: row-band x column-chunk walker, LDS row ring */
 };
 
 typedef struct iqo_hip_plan iqo_hip_plan;

@@ -39,6 +39,11 @@ struct iqo_hip_plan {
                             // streamer, 2: per-wave symmetric streamer
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
+    // tiled general streamer (shapes without a specialised kernel): ring rows, row pitch, taps
+    // off by default: on MI355X it is not yet faster than general_kernel (G1 2.30 vs 2.34 ms,
+    // G2 3.12 vs 1.98, G3 1.05 vs 1.16 ms per launch)
+    bool tileOk = false, useTile = false;
+    int tileR = 0, tilePitch = 0, tileTaps = 0, tileCp = 1;
 };
 
 namespace {
@@ -255,6 +260,40 @@ std::vector<int4> coord_records(const AxisPlan &a)
     return v;
 }
 
+// Ring geometry of the tiled general streamer: R = the largest per-row source window (rows),
+// pitch = the largest chunk span from its 16-B aligned start, rounded to 16 B; usable when the
+// workgroup's LDS stays within 64 KiB.
+void tile_geometry(iqo_hip_plan *h, const std::vector<int4> &chunks)
+{
+    const Plan &p = h->p;
+    int R = 1;
+    for (int y = 0; y < p.dstH; ++y) {
+        int s0, s1;
+        iqo_amd::band_src_rows(p, y, y + 1, &s0, &s1);
+        R = std::max(R, s1 - s0);
+    }
+    int pitch = 16;
+    for (const int4 &c : chunks)
+        pitch = std::max(pitch, ((c.w - (c.z & ~15)) + 15) & ~15);
+    const int taps = std::max(2, p.x.taps);  // per-thread X coefficients in LDS
+    int span = 0;
+    for (const int4 &c : chunks)
+        span = std::max(span, c.w - c.z);
+    int pow2 = 1;
+    while (pow2 < R)
+        pow2 *= 2;
+    R = pow2;  // slot = row & (R - 1)
+    int cp = 1;
+    while (256 * cp < span)
+        cp *= 2;
+    h->tileCp = cp;
+    const size_t lds = static_cast<size_t>(h->ldsInts + 256 * taps) * 4 + static_cast<size_t>(R) * pitch;
+    h->tileR = R;
+    h->tilePitch = pitch;
+    h->tileTaps = taps;
+    h->tileOk = lds <= 65536 && span <= 256 * 8 && p.kernel == IQO_KERNEL_GENERAL;
+}
+
 int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t dw, size_t dh, size_t px,
               int device, iqo_hip_plan **out)
 {
@@ -282,11 +321,13 @@ int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t d
     }
     std::vector<int4> chunks;
     int rc = build_chunks(h->p, &chunks, &h->ldsInts);
+    h->ldsInts = (h->ldsInts + 3) & ~3;  // keeps the tile streamer's ring 16-B aligned
     if (rc) {
         delete h;
         return rc;
     }
     h->nChunks = static_cast<int>(chunks.size());
+    tile_geometry(h, chunks);
     std::vector<int4> xr = coord_records(h->p.x), yr = coord_records(h->p.y);
     if ((rc = upload(&h->dX, xr.data(), xr.size())) || (rc = upload(&h->dY, yr.data(), yr.size())) ||
         (rc = upload(&h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
@@ -420,6 +461,8 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         kernel = IQO_KERNEL_GENERAL;
     if (kernel == IQO_KERNEL_LINEAR_UP2 && !(aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 16, dstSt, dstFrameSt)))
         kernel = IQO_KERNEL_GENERAL;
+    if (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tileOk && h->useTile)
+        kernel = IQO_KERNEL_TILE;
     return kernel;
 }
 
@@ -475,6 +518,9 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_area_int(area_dev(h), io, rb, re, s);
         else if (kernel == IQO_KERNEL_LINEAR_UP2)
             e = iqo_amd::launch_linear_up2(linear_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_TILE)
+            e = iqo_amd::launch_tile(general_dev(h), io, rb, re, h->tileR, h->tilePitch, h->tileTaps, h->tileCp,
+                                     aligned(io.src, 16, srcSt, srcFrameSt), s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -536,7 +582,9 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->tapsY = h->p.y.taps;
     d->phasesX = h->p.x.phases;
     d->phasesY = h->p.y.phases;
-    d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL : h->p.kernel;
+    d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL
+                                : (h->p.kernel == IQO_KERNEL_GENERAL && h->tileOk && h->useTile ? IQO_KERNEL_TILE
+                                                                                              : h->p.kernel);
     d->bandsPerFrame = h->bands;
     return IQO_HIP_OK;
 }
@@ -575,6 +623,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 62)
             return IQO_HIP_EINVAL;
         h->lanes = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "tile")) {  // 1: shapes without a specialised kernel use the tiled streamer
+        h->useTile = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "chunk_frames")) {  // frames per launch (0 = auto)
@@ -799,7 +851,8 @@ int iqo_hip_resize_yuv420_device(iqo_hip_yuv_plan *yp, size_t nFrames, size_t sr
     const int ky = kernel_for_layout(hy, srcY, srcStY, srcFrameSt, dstY, dstStY, dstFrameSt);
     const int ku = kernel_for_layout(hc, srcU, srcStUV, srcFrameSt, dstU, dstStUV, dstFrameSt);
     const int kv = kernel_for_layout(hc, srcV, srcStUV, srcFrameSt, dstV, dstStUV, dstFrameSt);
-    if (ky == ku && ku == kv && ky != IQO_KERNEL_GENERAL) {
+    if (ky == ku && ku == kv &&
+        (ky == IQO_KERNEL_LANCZOS_STREAM || ky == IQO_KERNEL_AREA_INT || ky == IQO_KERNEL_LINEAR_UP2)) {
         // frames per launch: as run_band
         size_t chunk = std::min<size_t>(65535, hy->chunkFrames > 0 ? static_cast<size_t>(hy->chunkFrames) : 65535);
         const size_t n = (nFrames + chunk - 1) / chunk;
@@ -915,11 +968,13 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
 {
     if (method < 0 || method > 2)
         return IQO_HIP_EINVAL;
-    Plan p;
+    iqo_hip_plan h;  // host half of a plan only: no device memory
     std::string err;
-    if (!iqo_amd::build_plan(static_cast<iqo_amd::Method>(method), degree, srcW, srcH, dstW, dstH, pxScale, &p, &err))
+    if (!iqo_amd::build_plan(static_cast<iqo_amd::Method>(method), degree, srcW, srcH, dstW, dstH, pxScale, &h.p, &err))
         return IQO_HIP_EINVAL;
-    return p.kernel;
+    if (h.p.kernel != IQO_KERNEL_GENERAL)
+        return h.p.kernel;
+    return IQO_KERNEL_GENERAL;  // the tiled streamer is opt-in (plan option "tile")
 }
 
 } // extern "C"

@@ -174,11 +174,16 @@ __device__ int y_value(const GeneralArgs &a, const uint8_t *srcF, int4 yi, int c
     return acc;
 }
 
-// Horizontal value at output column x from the LDS work row covering columns [lo, hi).
+// Horizontal value at output column x (record xi) from the LDS work row covering [lo, hi).
+__device__ int x_value_rec(const GeneralDev &g, const int *w, int lo, int hi, int x, int4 xi);
+
 __device__ int x_value(const GeneralArgs &a, const int *w, int lo, int hi, int x)
 {
-    const GeneralDev &g = a.g;
-    const int4 xi = g.xInfo[x];
+    return x_value_rec(a.g, w, lo, hi, x, a.g.xInfo[x]);
+}
+
+__device__ int x_value_rec(const GeneralDev &g, const int *w, int lo, int hi, int /*x*/, int4 xi)
+{
     auto W = [&](int col) { return w[max(0, min(col, hi - 1) - lo)]; };
     if (g.method == 0) {
         if (xi.z == KID)  // resizeX Y-only branch :520-527
@@ -235,6 +240,264 @@ __global__ __launch_bounds__(256) void general_kernel(GeneralArgs a)
         if (x < ch.y)
             dstRow[x] = static_cast<uint8_t>(x_value(a, wrow, ch.z, ch.w, x));
         __syncthreads();
+    }
+}
+
+// ================================================================ tiled general streamer
+//
+// Every shape the specialised kernels do not take (multi-phase ratios such as 1920 -> 1280,
+// Lanczos upscaling, non-integer Area, Linear at ratios other than 2x).  Same arithmetic as
+// general_kernel (y_value / x_value semantics, per-row and per-column coordinate records), but a
+// WORKGROUP walks a band of output rows for one column chunk and keeps the source rows it needs in
+// an LDS ring (ring slot = source row mod R), so each source byte is fetched from HBM about once
+// per (band, chunk) instead of once per tap.  Per output row: fetch the rows that entered the
+// window (coalesced buffer loads, 16 B per lane when the layout is 16-B aligned, else bytes),
+// stage the row's tap offsets and Y coefficients in LDS, compute the work row of the chunk's
+// source span into LDS, then one output per thread.
+
+constexpr int kTileAdv = 4;   // ... source rows entering the window per output row (prefetched)
+
+struct TileArgs {
+    GeneralDev g;
+    Io io;
+    int rowBegin, rowEnd, rowsPerBand;
+    int Rmask, pitch;   // ring rows - 1 (a power of two), bytes per ring row
+    int srcBytes;       // buffer range of one frame's source window
+    int maxTaps;        // capacity of the per-thread X coefficient array (>= nX)
+};
+
+// A record every lane reads at the same (uniform) address, made provably wave-uniform so that
+// everything derived from it lives in SGPRs and branches on it are scalar.
+__device__ __forceinline__ int4 uniform4(int4 v)
+{
+    return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+}
+
+// Source rows [a, b) that output row record yi reads (plan.cpp band_src_rows, per row).
+__device__ __forceinline__ void tile_row_window(const GeneralDev &g, int4 yi, int &a, int &b)
+{
+    if (yi.z == KID) {
+        a = yi.x;
+        b = yi.x + 1;
+    } else if (g.method == 2 && yi.z != KMAIN) {
+        a = yi.z == KLO ? 0 : g.srcH - 1;
+        b = a + 1;
+    } else {
+        a = yi.x;
+        b = yi.x + g.nY;
+    }
+    a = max(0, min(a, g.srcH - 1));
+    b = max(a + 1, min(b, g.srcH));
+}
+
+template <int VEC, int CP>
+__global__ __launch_bounds__(256) void tile_kernel(TileArgs t)
+{
+    // CP: work columns per thread, the chunk span rounded up (<= 256 * CP); extra columns are
+    // computed on clamped offsets and dropped.  The ring has a power-of-two row count (mask).
+    extern __shared__ __attribute__((aligned(16))) int tile_lds[];
+    const GeneralDev &g = t.g;
+    const int tid = static_cast<int>(threadIdx.x);
+    const int chunk = static_cast<int>(blockIdx.x) % g.nChunks;
+    const int band = static_cast<int>(blockIdx.x) / g.nChunks;
+    const int y0 = t.rowBegin + band * t.rowsPerBand;
+    const int y1 = min(y0 + t.rowsPerBand, t.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int4 ch = uniform4(g.chunks[chunk]);  // outputs [xs, xe), source span [lo, hi)
+    const int lo = ch.z, hi = ch.w;
+    const int base = VEC == 16 ? (lo & ~15) : lo;  // first column held by a ring row
+    const int nbytes = hi - base;
+    const int fullBytes = min(nbytes, (g.srcW - base) & ~15);
+    // LDS: work row [ldsInts] | X coefficients [nX][256] (this thread's taps) | ring
+    int *work = tile_lds;
+    int *xc = tile_lds + g.ldsInts;
+    uint8_t *ring = reinterpret_cast<uint8_t *>(xc + t.maxTaps * 256);
+
+    const __amdgpu_buffer_rsrc_t srcR = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(t.io.src + static_cast<int64_t>(blockIdx.y) * t.io.srcFrameSt), 0, t.srcBytes, 0x00020000);
+    uint8_t *dstF = t.io.dst + static_cast<int64_t>(blockIdx.y) * t.io.dstFrameSt;
+    const int srcSt = static_cast<int>(t.io.srcSt);
+
+    // this thread's output column, its record and its X coefficients (loop-invariant)
+    const int x = ch.x + tid;
+    const bool hasX = x < ch.y;
+    const int4 xi = hasX ? g.xInfo[x] : make_int4(0, 0, KID, 1);
+    const int nX = g.method == 2 ? 2 : g.nX;
+    for (int i = 0; i < nX; ++i)
+        xc[i * 256 + tid] = (hasX && xi.z != KID) ? g.tabX[xi.y + i] : 0;
+    // work columns of this thread: lo + tid + 256 k for k < kmax (ring offsets clamped into the span)
+    int colOff[CP];
+#pragma unroll
+    for (int k = 0; k < CP; ++k)
+        colOff[k] = min(lo + tid + 256 * k, hi - 1) - base;
+    auto W = [&](int col) { return work[max(0, min(col, hi - 1) - lo)]; };
+
+    // Source rows reach the ring one output row ahead: the rows that enter the window of row y+1
+    // (at most kTileAdv) are loaded into registers while row y is computed, and written to the
+    // ring at the start of row y+1.  The first row of the band loads its window directly.
+    // 16-B aligned layouts only (VEC == 16); the byte path loads each row when it is needed.
+    auto load_row_now = [&](int r) {
+        uint8_t *dr = ring + (r & t.Rmask) * t.pitch;
+        const int so = (r - t.io.srcRow0) * srcSt + base;
+        if constexpr (VEC == 16) {
+            // whole 16-B blocks inside the row (a block crossing the end of the frame's last
+            // row would be out of range as a whole and read as zeros), then the tail bytes
+            for (int off = tid * 16; off < fullBytes; off += 256 * 16) {
+                u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srcR, off, so, 0);
+                *reinterpret_cast<u32x4 *>(dr + off) = v;
+            }
+            for (int off = fullBytes + tid; off < nbytes; off += 256)
+                dr[off] = __builtin_amdgcn_raw_buffer_load_b8(srcR, off, so, 0);
+        } else {
+            for (int off = tid; off < nbytes; off += 256)
+                dr[off] = __builtin_amdgcn_raw_buffer_load_b8(srcR, off, so, 0);
+        }
+    };
+    u32x4 pf[kTileAdv];  // prefetched 16-B block of row (have1 + j) for this thread
+    uint32_t pfb[kTileAdv];  // ... and one tail byte
+    int nPf = 0;  // rows in the prefetch registers (uniform)
+    const int blk = tid * 16, tailOff = fullBytes + tid;
+    int have1 = INT_MIN;  // source rows [window start, have1) are resident
+    for (int y = y0; y < y1; ++y) {
+        const int4 yi = uniform4(g.yInfo[y]);
+        int ra, rb;
+        tile_row_window(g, yi, ra, rb);
+        if (VEC == 16 && y > y0) {
+            // the rows prefetched during the previous output row ([have1, have1 + nPf) == [.., rb))
+#pragma unroll
+            for (int j = 0; j < kTileAdv; ++j)
+                if (j < nPf) {
+                    uint8_t *dr = ring + ((have1 + j) & t.Rmask) * t.pitch;
+                    if (blk < fullBytes)
+                        *reinterpret_cast<u32x4 *>(dr + blk) = pf[j];
+                    if (tailOff < nbytes)
+                        dr[tailOff] = static_cast<uint8_t>(pfb[j]);
+                }
+            // rows beyond the prefetch depth (steep downscales) come in now
+            for (int r = max(ra, have1 + kTileAdv); r < rb; ++r)
+                load_row_now(r);
+        } else {
+            for (int r = max(ra, have1); r < rb; ++r)
+                load_row_now(r);
+        }
+        have1 = rb;
+        if (VEC == 16 && y + 1 < y1) {
+            // prefetch the rows entering the next output row's window
+            const int4 yn = uniform4(g.yInfo[y + 1]);
+            int rn0, rn1;
+            tile_row_window(g, yn, rn0, rn1);
+            nPf = min(kTileAdv, max(0, rn1 - max(rb, rn0)));
+            const int r0 = max(rb, rn0);
+            if (rn0 > rb)
+                have1 = INT_MIN;  // the next window jumps past this one: nothing carries over
+#pragma unroll
+            for (int j = 0; j < kTileAdv; ++j)
+                if (j < nPf) {
+                    const int so = (r0 + j - t.io.srcRow0) * srcSt + base;
+                    if (blk < fullBytes)
+                        pf[j] = __builtin_amdgcn_raw_buffer_load_b128(srcR, blk, so, 0);
+                    if (tailOff < nbytes)
+                        pfb[j] = __builtin_amdgcn_raw_buffer_load_b8(srcR, tailOff, so, 0);
+                }
+            if (rn0 > rb)
+                have1 = r0;  // written at the next row's start as rows [r0, r0 + nPf)
+        }
+        __syncthreads();  // ring rows visible; the previous row's outputs are done
+
+        // vertical (general_kernel y_value): int32 sums, truncated to the reference's int16 / u16
+        // work type at the end (wrapping sums are exact mod 2^16).  Taps are uniform: row, ring
+        // slot and coefficient come from scalar registers; rows outside the image weigh 0.
+        int acc[CP];
+#pragma unroll
+        for (int k = 0; k < CP; ++k)
+            acc[k] = 0;
+        if (yi.z == KID || (g.method == 2 && yi.z != KMAIN)) {
+            // identity rows / Linear replicated border rows: the single window row times B
+            const int so = (ra & t.Rmask) * t.pitch;
+#pragma unroll
+            for (int k = 0; k < CP; ++k)
+                acc[k] = ring[so + colOff[k]] * (g.method == 0 ? 64 : 256);
+        } else {
+            const int nT = g.method == 2 ? 2 : g.nY;
+            for (int i = 0; i < nT; ++i) {
+                int r = yi.x + i;
+                if (g.method == 2)
+                    r = max(0, min(r, g.srcH - 1));  // Linear main: rows clamp(o), clamp(o + 1)
+                else if (g.method == 1)
+                    r = min(r, g.srcH - 1);  // Area: weight-0 tap past the end clamped
+                const bool in = r >= 0 && r < g.srcH;
+                const int c = in ? __builtin_amdgcn_readfirstlane(g.tabY[yi.y + i]) : 0;
+                const int so = (in ? r & t.Rmask : 0) * t.pitch;
+#pragma unroll
+                for (int k = 0; k < CP; ++k)
+                    acc[k] += ring[so + colOff[k]] * c;
+            }
+        }
+        const bool border = g.method == 0 && yi.z != KMAIN && yi.z != KID;
+#pragma unroll
+        for (int k = 0; k < CP; ++k) {
+            const int col = lo + tid + 256 * k;
+            if (col < hi) {
+                int v;
+                if (g.method == 0) {
+                    v = static_cast<int16_t>(acc[k]);  // resizeYmain :509-515 (int16 wrap)
+                    if (border)  // resizeYborder :477-489
+                        v = static_cast<int16_t>(exact_div(v * 64, yi.w));
+                } else {
+                    v = static_cast<uint16_t>(acc[k]);
+                }
+                work[col - lo] = v;
+            }
+        }
+        __syncthreads();
+
+        // horizontal (general_kernel x_value), coefficients from LDS
+        if (hasX) {
+            int out;
+            if (g.method == 0) {
+                if (xi.z == KID) {
+                    out = clamp255(static_cast<int16_t>((W(xi.x) + 32) >> 6));
+                } else if (xi.z == KMAIN) {
+                    int sum = 0;  // resizeXmain :605-610
+                    for (int i = 0; i < nX; ++i)
+                        sum += W(xi.x + i) * xc[i * 256 + tid];
+                    out = clamp255(static_cast<int16_t>((sum + (1 << 19)) >> 20));
+                } else {
+                    int nume = 0;  // resizeXborder :563-572
+                    for (int i = 0; i < nX; ++i) {
+                        const int col = xi.x + i;
+                        if (col >= 0 && col < g.srcW)
+                            nume += W(col) * xc[i * 256 + tid];
+                    }
+                    out = clamp255(static_cast<int16_t>(exact_div(nume + (1 << 19), xi.w * 64)));
+                }
+            } else {
+                auto u16clamp = [](int v) {  // uint8(clamp<uint16_t>(0, 255, int16(v)))
+                    uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(v));
+                    return static_cast<int>(u > 255 ? 255 : u);
+                };
+                if (xi.z == KID) {
+                    out = clamp255(static_cast<int16_t>((W(xi.x) + 128) >> 8));
+                } else if (g.method == 1) {  // Area resizeXmain :349-367
+                    int sum = 0;
+                    for (int i = 0; i < nX; ++i)
+                        sum += W(min(xi.x + i, g.srcW - 1)) * xc[i * 256 + tid];
+                    out = u16clamp((sum + (1 << 22)) >> 23);
+                } else if (xi.z == KLO) {  // Linear resizeXborder :355-366
+                    out = u16clamp((W(0) + 128) >> 8);
+                } else if (xi.z == KHI) {
+                    out = u16clamp((W(g.srcW - 1) + 128) >> 8);
+                } else {
+                    const int c0 = max(0, min(xi.x, g.srcW - 1)), c1 = max(0, min(xi.x + 1, g.srcW - 1));
+                    out = u16clamp((W(c0) * xc[tid] + W(c1) * xc[256 + tid] + (1 << 22)) >> 23);  // :400-405
+                }
+            }
+            dstF[static_cast<int64_t>(y - t.io.dstRow0) * t.io.dstSt + x] = static_cast<uint8_t>(out);
+        }
+        // the next row's loads touch only ring rows this row no longer reads (capacity R >= the
+        // largest window); the barrier after them orders the work-row rewrite
     }
 }
 
@@ -1441,6 +1704,38 @@ hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int r
     size_t lds = static_cast<size_t>(g.ldsInts) * sizeof(int);
     hipLaunchKernelGGL(general_kernel, grid, dim3(256), lds, s, a);
     return hipGetLastError();
+}
+
+hipError_t launch_tile(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, int R, int pitch, int maxTaps,
+                       int cp, bool vec16, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    const int rows = rowEnd - rowBegin;
+    const int64_t sb = static_cast<int64_t>(g.srcH - io.srcRow0 - 1) * io.srcSt + g.srcW;
+    if (sb >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 31))
+        return hipErrorInvalidValue;
+    const size_t lds = static_cast<size_t>(g.ldsInts + 256 * maxTaps) * sizeof(int) + static_cast<size_t>(R) * pitch;
+    // bands: enough workgroups for ~8 per CU over the batch, at least 8 rows per band (each band
+    // start re-reads its window)
+    const int64_t perBand = static_cast<int64_t>(g.nChunks) * io.frames;
+    int bands = static_cast<int>(std::max<int64_t>(1, (2048 + perBand - 1) / perBand));
+    bands = std::max(1, std::min(bands, rows / 8 > 0 ? rows / 8 : 1));
+    const int rpb = (rows + bands - 1) / bands;
+    bands = (rows + rpb - 1) / rpb;
+    TileArgs t{g, io, rowBegin, rowEnd, rpb, R - 1, pitch, static_cast<int>(sb), maxTaps};
+    dim3 grid(static_cast<unsigned>(bands * g.nChunks), static_cast<unsigned>(io.frames));
+    void *args[] = {&t};
+    const int span = cp;  // 1, 2, 4 or 8 columns per thread
+    const void *kern = nullptr;
+#define IQO_TILE(V)                                                                                     \
+    (span <= 1 ? reinterpret_cast<const void *>(tile_kernel<V, 1>)                                     \
+               : span <= 2 ? reinterpret_cast<const void *>(tile_kernel<V, 2>)                         \
+                           : span <= 4 ? reinterpret_cast<const void *>(tile_kernel<V, 4>)             \
+                                       : reinterpret_cast<const void *>(tile_kernel<V, 8>))
+    kern = vec16 ? IQO_TILE(16) : IQO_TILE(1);
+#undef IQO_TILE
+    return hipLaunchKernel(kern, grid, dim3(256), args, lds, s);
 }
 
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)

@@ -29,6 +29,11 @@ struct GeneralDev {
     int ldsInts;                 // work-row capacity (ints) of the largest chunk
 };
 hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
+// --- tiled general streamer: same semantics, a workgroup walks a band of rows of one chunk with
+// the source rows in an LDS ring of R rows x pitch bytes (R a power of two >= the largest per-row
+// window); cp = work columns per thread (1, 2, 4, 8: the largest chunk span / 256, rounded up).
+hipError_t launch_tile(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, int R, int pitch, int maxTaps,
+                       int cp, bool vec16, hipStream_t s);
 
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {

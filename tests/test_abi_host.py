@@ -103,6 +103,8 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "general"),
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "general"),
     (("area", 0, 1920, 1080, 1280, 720, 1), "general"),
+    (("lanczos", 3, 1920, 1080, 960, 540, 2), "lanczos_stream"),   # pxScale-2 chroma (ring streamer)
+    (("lanczos", 9, 4000, 3000, 97, 61, 1), "general"),
 ])
 def test_fast_path_selection(cfg, kernel):
     assert libiqo_amd.host_kernel_for(*cfg) == kernel

@@ -39,16 +39,20 @@ def test_native_library_is_the_gpu_path():
     assert r.describe()["kernel"] == "lanczos_stream"
 
 
-@pytest.mark.parametrize("force_general", [False, True])
+@pytest.mark.parametrize("force_general", [False, True, "tile"])
 def test_golden_vectors_gpu(golden, force_general):
-    """Every golden case, via the host-pointer entry point (reference resize() semantics)."""
+    """Every golden case, via the host-pointer entry point (reference resize() semantics): default
+    kernels, the reference general_kernel, and the opt-in tiled streamer for every shape without a
+    specialised kernel."""
     n = 0
     for c in golden["cases"]:
         sw, sh, dw, dh = c["srcW"], c["srcH"], c["dstW"], c["dstH"]
         if sw * sh > 4_000_000:
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
-        if force_general:
+        if force_general == "tile":
+            r.set_option("tile", 1)
+        elif force_general:
             r.set_option("force_general", 1)
         src = ol.gen(c["gen"], sw, sh, c["seed"])
         out = _run_host(r, src, dw, dh)
@@ -216,6 +220,49 @@ def test_chroma_pxscale2_stream_agrees_with_oracle(shape):
         for f in range(2):
             bad = np.argwhere(out[f] != exp[f])
             assert bad.size == 0, (shape, pd, bands, f, bad[:4].tolist())
+
+
+TILE_SHAPES = [
+    ("lanczos", 3, 1920, 1080, 1280, 720, 1),   # 3:2, 2 phases
+    ("lanczos", 3, 640, 480, 1280, 960, 1),     # upscale
+    ("lanczos", 2, 1000, 700, 333, 250, 1),     # odd ratios, borders everywhere
+    ("lanczos", 4, 801, 601, 400, 300, 2),      # pxScale 2, 2:1 odd sizes
+    ("area", 0, 1920, 1080, 1280, 720, 1),      # non-integer area (weight-0 tap past the end)
+    ("linear", 0, 640, 480, 1000, 700, 1),      # linear, non-2x
+    ("lanczos", 3, 64, 48, 640, 480, 1),        # 10x upscale
+    ("lanczos", 3, 3840, 2160, 3840, 1080, 1),  # Y only (X identity)
+]
+
+
+@pytest.mark.parametrize("cfg", TILE_SHAPES, ids=lambda c: "%s%d_%dx%d_%dx%d" % c[:6])
+def test_tile_streamer_matches_oracle(cfg):
+    """The tiled general streamer (shapes without a specialised kernel) equals the oracle, with the
+    16-B and the byte load paths (aligned and misaligned bases), and equals the reference
+    general_kernel (tile off) on the same batch."""
+    m, d, sw, sh, dw, dh, px = cfg
+    frames = _noise_batch(2, sw, sh, 1100)
+    frames[1, :, : sw // 3] = 255
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    r.set_option("tile", 1)  # opt-in (not yet faster than general_kernel)
+    assert r.describe()["kernel"] == "tile"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(2):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    # misaligned base (byte loads), padded strides
+    sst = sw + 3
+    sbuf = torch.zeros(sh * sst + 64, dtype=torch.uint8, device=DEV)
+    sview = sbuf[1:1 + sh * sst].view(sh, sst)
+    sview[:, :sw] = src[0]
+    dbuf = torch.zeros(dh * (dw + 5), dtype=torch.uint8, device=DEV)
+    r.resize_device(1, sst, sh * sst, sview.data_ptr(), dw + 5, dh * (dw + 5), dbuf.data_ptr())
+    got = dbuf.view(dh, dw + 5)[:, :dw].cpu().numpy()
+    assert (got == exp[0]).all(), cfg
+    g = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert g.describe()["kernel"] == "general"
+    assert torch.equal(g.resize_tensor(src), r.resize_tensor(src))
 
 
 LINEAR_UP2_SHAPES = [
