@@ -1054,6 +1054,9 @@ template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
 #ifndef IQO_SYMB_WAVES_PER_EU
 #define IQO_SYMB_WAVES_PER_EU 4
 #endif
+#ifndef IQO_SYMB_LA
+#define IQO_SYMB_LA 1  // LDS look-ahead in the block-shared streamer (C2: ~1% faster)
+#endif
 #ifndef IQO_SYMB_EDGE_BATCH
 #define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (C2: 64 -> 16 cuts write traffic +4.5% -> +2%)
 #endif
@@ -1063,6 +1066,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
     static_assert(K >= 2 && CPW >= 1, "ring depth");
     constexpr int WAIT = 1 + (K - 2) * (2 * CPW + 1);  // vm ops issued after this wave's DMA(i)
+#if IQO_SYMB_LA
+    // LDS look-ahead: iteration i reads the ring slot of iteration i+1 (its latency hides behind
+    // iteration i's arithmetic), so it waits for DMA(i+1): one fewer DMA iteration in flight
+    static_assert(K >= 3, "look-ahead needs K >= 3");
+    constexpr int WAITLA = 1 + (K - 3) * (2 * CPW + 1);
+#endif
     constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
     constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
     static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
@@ -1206,12 +1215,31 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, 0x7ff00000, 0, 0);
     }
 
+#if IQO_SYMB_LA
+    uint4 n0, n1;  // this iteration's two new rows (read from LDS one iteration ahead)
+    wait_vmcnt<WAIT>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_iter(0, n0, n1);
+#endif
     auto row = [&](auto uc, int base) {
         constexpr int v = decltype(uc)::value;
         const int i = base + v;  // iteration = output row y0 + i
         if (i >= nRows)
             return;  // past the band end (uniform)
         const int yy = dir > 0 ? y0 + i : y1 - 1 - i;
+#if IQO_SYMB_LA
+        // this wave's DMA(i+1) retired (WAITLA younger vm ops); the barrier publishes slot i+1
+        // and retires every wave's reads of slot i-1, which DMA(i+K-1) refills
+        wait_vmcnt<WAITLA>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        uint4 m0, m1;
+        read_iter(i + 1, m0, m1);
+        dma_iter(i + K - 1);
+#else
         // this wave's DMA(i) retired: after it come the store of iteration i-K+1 and the 2*CPW
         // DMAs + 1 store of each of iterations i-K+2 .. i-1; then the workgroup barrier makes
         // every wave's chunks of iteration i visible and retires all reads of slot (i-1) mod K
@@ -1220,11 +1248,14 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 #endif
         wait_vmcnt<WAIT>();
         asm volatile("" ::: "memory");
+#ifndef IQO_EXP_NOBARRIER  // timing experiment only (races: wrong output)
         __builtin_amdgcn_s_barrier();
+#endif
         asm volatile("" ::: "memory");
         uint4 n0, n1;
         read_iter(i, n0, n1);
         dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
+#endif
 #ifdef IQO_EXP_SETPRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1235,6 +1266,10 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 #endif
         unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
         unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
+#if IQO_SYMB_LA
+        n0 = m0;
+        n1 = m1;
+#endif
 
         // vertical: pair p = slots (2v + p, 2v + NY - 1 - p) mod NY
         uint32_t acc[8];
