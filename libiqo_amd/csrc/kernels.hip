@@ -1054,6 +1054,9 @@ template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
 #ifndef IQO_SYMB_WAVES_PER_EU
 #define IQO_SYMB_WAVES_PER_EU 4
 #endif
+#ifndef IQO_SYMB_DPPDOT
+#define IQO_SYMB_DPPDOT 1  // neighbour pairs through DPP-modified v_dot2c (C2: ~1% faster)
+#endif
 #ifndef IQO_SYMB_LA
 #define IQO_SYMB_LA 1  // LDS look-ahead in the block-shared streamer (C2: ~1% faster)
 #endif
@@ -1121,6 +1124,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;  // last source row the band reads
     const int nRows = y1 - y0;
     const uint32_t bias = opaque(1u << 19);            // rounding bias (VOP3P src2 of the first dot)
+#if IQO_SYMB_DPPDOT
+    uint32_t cvx[NX / 2];  // X coefficient pairs in VGPRs (VOP2 DPP needs a VGPR src1)
+#pragma unroll
+    for (int p = 0; p < NX / 2; ++p)
+        cvx[p] = opaque(L.cxo[p]);
+#endif
 
     // shared LDS ring: iteration i's two walk rows live in slot i mod K; chunk c (1 KiB of
     // source columns [1024c, 1024c + 1024) at LDS column 16 + 1024c) is DMA'd by wave c mod wpr
@@ -1296,6 +1305,43 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                 acc[c] = ydiv2(acc[c], m, sh);
         }
 
+        int sum[8];
+#if IQO_SYMB_DPPDOT
+        // neighbour pairs enter the dot products through the DPP source modifier of
+        // v_dot2c_i32_i16 (no separate v_mov_dpp); each output starts with an own pair (VOP3P form,
+        // the bias VGPR as src2).  s_nop 1: DPP reads of VGPRs the vertical pass just wrote.
+        asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            int pFirst = -1;  // first tap whose pair is this lane's own
+#pragma unroll
+            for (int p = 0; p < NX / 2; ++p) {
+                const int j = k + p + JLO;
+                if (pFirst < 0 && j >= 1 && j <= 8)
+                    pFirst = p;
+            }
+            int sacc;
+            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[pFirst]), "v"(acc[k + pFirst + JLO - 1]),
+                "v"(bias));
+#pragma unroll
+            for (int p = 0; p < NX / 2; ++p) {
+                const int j = k + p + JLO;
+                if (p == pFirst)
+                    continue;
+                if (j <= 0)
+                    asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+                        : "+v"(sacc) : "v"(acc[j + 7]), "v"(cvx[p]));
+                else if (j >= 9)
+                    asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf"
+                        : "+v"(sacc) : "v"(acc[j - 9]), "v"(cvx[p]));
+                else
+                    sacc = sdot2(acc[j - 1], L.cxo[p], sacc);
+            }
+            sum[k] = sacc;
+        }
+#else
         // Q_j for j in [JLO, JHI): own pairs 1..8, neighbours' by DPP
         uint32_t q[JHI - JLO];
 #pragma unroll
@@ -1309,7 +1355,6 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             else
                 q[j - JLO] = acc[j - 1];
         }
-        int sum[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             int sacc;  // VOP3P form: the bias VGPR is src2, no copy into the accumulator
@@ -1319,6 +1364,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                 sacc = sdot2(q[k + p], L.cxo[p], sacc);
             sum[k] = sacc;
         }
+#endif
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
