@@ -36,7 +36,7 @@ struct iqo_hip_plan {
     int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
     int linPrefetch = 0;    // Linear 2x streamer: source rows in flight per wave (0 = default 2)
     int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
-                            // streamer, 2: per-wave symmetric streamer
+                            // streamer, 2: per-wave symmetric streamer, 3: half-width block-shared
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // tiled general streamer (shapes without a specialised kernel): ring rows, row pitch, taps
@@ -386,7 +386,7 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.xNeg = f.xNeg;
     l.dbg = h->debugFlags;
     l.prefetch = h->prefetch;
-    l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant == 2 ? 2 : 1);
+    l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
     l.NX = f.NX;
     l.offXO = f.offXO;
     for (int i = 0; i < f.NX / 2 && i < 8; ++i)
@@ -614,7 +614,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric block-shared (default), 1 ring,
-        if (value < 0 || value > 2)              // 2 symmetric per-wave
+        if (value < 0 || value > 3)              // 2 symmetric per-wave, 3 half-width block-shared
             return IQO_HIP_EINVAL;
         h->streamVariant = static_cast<int>(value);
         return IQO_HIP_OK;

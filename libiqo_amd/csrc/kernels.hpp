@@ -51,7 +51,7 @@ struct LanczosDev {
     int dbg;                     // timing experiments only (see kernels.hip)
     int prefetch;                // prefetch depth in output rows (1..3)
     // symmetric streamer (plan.hpp FastLanczos::sym)
-    int sym;                     // 1: block-shared symmetric, 2: per-wave symmetric, 0: accumulator ring
+    int sym;                     // 1: block-shared symmetric, 2: per-wave symmetric, 3: half-width block-shared, 0: accumulator ring
     int NX, offXO;               // unpadded X taps, odd first tap column
     uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table
     int np;                      // producing lanes per wave (0 = auto)

@@ -171,8 +171,9 @@ STREAM_SHAPES = [
 
 @pytest.mark.parametrize("shape", STREAM_SHAPES, ids=lambda s: "L%d_%dx%d" % s[:3])
 def test_stream_variants_agree_with_oracle(shape):
-    """Every Lanczos streamer (block-shared symmetric, accumulator ring, per-wave symmetric), every
-    prefetch depth, forced lane counts and band splits produce the oracle's output."""
+    """Every Lanczos streamer (block-shared symmetric at full and half lane width, accumulator ring,
+    per-wave symmetric), every prefetch depth, forced lane counts and band splits produce the
+    oracle's output."""
     d, sw, sh, dw, dh = shape
     frames = _noise_batch(2, sw, sh, 300)
     frames[1, :, : sw // 5] = 255
@@ -180,7 +181,7 @@ def test_stream_variants_agree_with_oracle(shape):
     exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 1, frames[f]) for f in range(2)]
     for variant, pd, lanes, bands in [(0, 1, 0, 0), (0, 2, 0, 7), (0, 3, 0, 0), (0, 2, 62, 3), (0, 3, 33, 0),
                                       (0, 3, 0, 1), (1, 3, 0, 0), (1, 1, 0, 5), (2, 3, 0, 0), (2, 1, 0, 5),
-                                      (2, 2, 40, 0)]:
+                                      (2, 2, 40, 0), (3, 3, 0, 0), (3, 2, 0, 7), (3, 3, 41, 0), (3, 3, 0, 1)]:
         r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
         assert r.describe()["kernel"] == "lanczos_stream"
         r.set_option("stream_variant", variant)
