@@ -54,7 +54,7 @@ enum {
     IQO_KERNEL_LANCZOS_STREAM = 1, /* integer ratio, 1 phase: row-band walker, register window */
     IQO_KERNEL_AREA_INT = 2,    /* integer ratio area */
     IQO_KERNEL_LINEAR_UP2 = 3,  /* exact 2x bilinear upsampling */
-    IQO_KERNEL_TILE = 4         /* any other shape: row-band x column-chunk walker, LDS row ring */
+    IQO_KERNEL_TILE = 4         /* any other shape: separable tiles (TH rows x CT columns, work rows in LDS) */
 };
 
 typedef struct iqo_hip_plan iqo_hip_plan;

@@ -39,11 +39,13 @@ struct iqo_hip_plan {
                             // streamer, 2: per-wave symmetric streamer, 3: half-width block-shared
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
-    // tiled general streamer (shapes without a specialised kernel): ring rows, row pitch, taps
-    // off by default: on MI355X it is not yet faster than general_kernel (G1 2.30 vs 2.34 ms,
-    // G2 3.12 vs 1.98, G3 1.05 vs 1.16 ms per launch)
-    bool tileOk = false, useTile = false;
-    int tileR = 0, tilePitch = 0, tileTaps = 0, tileCp = 1;
+    // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
+    // it off, leaving general_kernel)
+    iqo_amd::TileTables tt;
+    bool useTile = true;
+    int4 *dTRows = nullptr, *dTSpans = nullptr;
+    int2 *dTCols = nullptr;
+    uint32_t *dTRowCoef = nullptr, *dTColCoef = nullptr;
 };
 
 namespace {
@@ -249,6 +251,11 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dChunks);
     (void)hipFree(h->dTabX);
     (void)hipFree(h->dTabY);
+    (void)hipFree(h->dTRows);
+    (void)hipFree(h->dTCols);
+    (void)hipFree(h->dTSpans);
+    (void)hipFree(h->dTRowCoef);
+    (void)hipFree(h->dTColCoef);
     delete h;
 }
 
@@ -260,38 +267,27 @@ std::vector<int4> coord_records(const AxisPlan &a)
     return v;
 }
 
-// Ring geometry of the tiled general streamer: R = the largest per-row source window (rows),
-// pitch = the largest chunk span from its 16-B aligned start, rounded to 16 B; usable when the
-// workgroup's LDS stays within 64 KiB.
-void tile_geometry(iqo_hip_plan *h, const std::vector<int4> &chunks)
+// Upload the separable tile kernel's tables (TileRec / TileCol have the int4 / int2 layout).
+int upload_tile(iqo_hip_plan *h)
 {
-    const Plan &p = h->p;
-    int R = 1;
-    for (int y = 0; y < p.dstH; ++y) {
-        int s0, s1;
-        iqo_amd::band_src_rows(p, y, y + 1, &s0, &s1);
-        R = std::max(R, s1 - s0);
-    }
-    int pitch = 16;
-    for (const int4 &c : chunks)
-        pitch = std::max(pitch, ((c.w - (c.z & ~15)) + 15) & ~15);
-    const int taps = std::max(2, p.x.taps);  // per-thread X coefficients in LDS
-    int span = 0;
-    for (const int4 &c : chunks)
-        span = std::max(span, c.w - c.z);
-    int pow2 = 1;
-    while (pow2 < R)
-        pow2 *= 2;
-    R = pow2;  // slot = row & (R - 1)
-    int cp = 1;
-    while (256 * cp < span)
-        cp *= 2;
-    h->tileCp = cp;
-    const size_t lds = static_cast<size_t>(h->ldsInts + 256 * taps) * 4 + static_cast<size_t>(R) * pitch;
-    h->tileR = R;
-    h->tilePitch = pitch;
-    h->tileTaps = taps;
-    h->tileOk = lds <= 65536 && span <= 256 * 8 && p.kernel == IQO_KERNEL_GENERAL;
+    const iqo_amd::TileTables &t = h->tt;
+    if (!t.ok)
+        return IQO_HIP_OK;
+    std::vector<int4> rows(t.rows.size()), spans(t.spans.size());
+    std::vector<int2> cols(t.cols.size());
+    for (size_t i = 0; i < rows.size(); ++i)
+        rows[i] = make_int4(t.rows[i].start, t.rows[i].lo, t.rows[i].hi, t.rows[i].deno);
+    for (size_t i = 0; i < cols.size(); ++i)
+        cols[i] = make_int2(t.cols[i].a, t.cols[i].D);
+    for (size_t i = 0; i < spans.size(); ++i)
+        spans[i] = make_int4(t.spans[i].lo8, t.spans[i].groups, 0, 0);
+    int rc;
+    if ((rc = upload(&h->dTRows, rows.data(), rows.size())) || (rc = upload(&h->dTCols, cols.data(), cols.size())) ||
+        (rc = upload(&h->dTSpans, spans.data(), spans.size())) ||
+        (rc = upload(&h->dTRowCoef, t.rowCoef.data(), t.rowCoef.size())) ||
+        (rc = upload(&h->dTColCoef, t.colCoef.data(), t.colCoef.size())))
+        return rc;
+    return IQO_HIP_OK;
 }
 
 int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t dw, size_t dh, size_t px,
@@ -321,18 +317,17 @@ int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t d
     }
     std::vector<int4> chunks;
     int rc = build_chunks(h->p, &chunks, &h->ldsInts);
-    h->ldsInts = (h->ldsInts + 3) & ~3;  // keeps the tile streamer's ring 16-B aligned
     if (rc) {
         delete h;
         return rc;
     }
     h->nChunks = static_cast<int>(chunks.size());
-    tile_geometry(h, chunks);
+    iqo_amd::build_tile_tables(h->p, &h->tt);
     std::vector<int4> xr = coord_records(h->p.x), yr = coord_records(h->p.y);
     if ((rc = upload(&h->dX, xr.data(), xr.size())) || (rc = upload(&h->dY, yr.data(), yr.size())) ||
         (rc = upload(&h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
         (rc = upload(&h->dTabY, h->p.y.table.data(), h->p.y.table.size())) ||
-        (rc = upload(&h->dChunks, chunks.data(), chunks.size()))) {
+        (rc = upload(&h->dChunks, chunks.data(), chunks.size())) || (rc = upload_tile(h))) {
         free_plan(h);
         return rc;
     }
@@ -428,6 +423,28 @@ iqo_amd::LinearDev linear_dev(const iqo_hip_plan *h)
     return l;
 }
 
+iqo_amd::TileDev tile_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::TileTables &t = h->tt;
+    iqo_amd::TileDev d;
+    d.lanczos = h->p.method == iqo_amd::kLanczos;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.NP = t.NP;
+    d.nYp = t.nYp;
+    d.CT = t.CT;
+    d.TH = t.TH;
+    d.pitchDw = t.pitchDw;
+    d.log2nQ = t.log2nQ;
+    d.rows = h->dTRows;
+    d.rowCoef = h->dTRowCoef;
+    d.cols = h->dTCols;
+    d.colCoef = h->dTColCoef;
+    d.spans = h->dTSpans;
+    return d;
+}
+
 iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
 {
     const Plan &p = h->p;
@@ -461,8 +478,8 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         kernel = IQO_KERNEL_GENERAL;
     if (kernel == IQO_KERNEL_LINEAR_UP2 && !(aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 16, dstSt, dstFrameSt)))
         kernel = IQO_KERNEL_GENERAL;
-    if (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tileOk && h->useTile)
-        kernel = IQO_KERNEL_TILE;
+    if (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tt.ok && h->useTile)
+        kernel = IQO_KERNEL_TILE;  // any alignment (the kernel adapts per frame)
     return kernel;
 }
 
@@ -519,8 +536,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
         else if (kernel == IQO_KERNEL_LINEAR_UP2)
             e = iqo_amd::launch_linear_up2(linear_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_TILE)
-            e = iqo_amd::launch_tile(general_dev(h), io, rb, re, h->tileR, h->tilePitch, h->tileTaps, h->tileCp,
-                                     aligned(io.src, 16, srcSt, srcFrameSt), s);
+            e = iqo_amd::launch_tile(tile_dev(h), io, rb, re, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -583,7 +599,7 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->phasesX = h->p.x.phases;
     d->phasesY = h->p.y.phases;
     d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL
-                                : (h->p.kernel == IQO_KERNEL_GENERAL && h->tileOk && h->useTile ? IQO_KERNEL_TILE
+                                : (h->p.kernel == IQO_KERNEL_GENERAL && h->tt.ok && h->useTile ? IQO_KERNEL_TILE
                                                                                               : h->p.kernel);
     d->bandsPerFrame = h->bands;
     return IQO_HIP_OK;
@@ -625,7 +641,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->lanes = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "tile")) {  // 1: shapes without a specialised kernel use the tiled streamer
+    if (!std::strcmp(key, "tile")) {  // 0: shapes without a specialised kernel use general_kernel
         h->useTile = value != 0;
         return IQO_HIP_OK;
     }
@@ -974,7 +990,8 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
         return IQO_HIP_EINVAL;
     if (h.p.kernel != IQO_KERNEL_GENERAL)
         return h.p.kernel;
-    return IQO_KERNEL_GENERAL;  // the tiled streamer is opt-in (plan option "tile")
+    iqo_amd::build_tile_tables(h.p, &h.tt);
+    return h.tt.ok ? IQO_KERNEL_TILE : IQO_KERNEL_GENERAL;
 }
 
 } // extern "C"

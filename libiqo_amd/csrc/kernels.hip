@@ -25,6 +25,7 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 
 // 16-byte streaming load (source pixels are read once per band): nontemporal hint.
 __device__ __forceinline__ uint4 load16_nt(const uint8_t *p)
@@ -243,261 +244,191 @@ __global__ __launch_bounds__(256) void general_kernel(GeneralArgs a)
     }
 }
 
-// ================================================================ tiled general streamer
+// ================================================================ separable tile kernel
 //
-// Every shape the specialised kernels do not take (multi-phase ratios such as 1920 -> 1280,
-// Lanczos upscaling, non-integer Area, Linear at ratios other than 2x).  Same arithmetic as
-// general_kernel (y_value / x_value semantics, per-row and per-column coordinate records), but a
-// WORKGROUP walks a band of output rows for one column chunk and keeps the source rows it needs in
-// an LDS ring (ring slot = source row mod R), so each source byte is fetched from HBM about once
-// per (band, chunk) instead of once per tap.  Per output row: fetch the rows that entered the
-// window (coalesced buffer loads, 16 B per lane when the layout is 16-B aligned, else bytes),
-// stage the row's tap offsets and Y coefficients in LDS, compute the work row of the chunk's
-// source span into LDS, then one output per thread.
-
-constexpr int kTileAdv = 4;   // ... source rows entering the window per output row (prefetched)
+// Every shape the specialised kernels do not take: multi-phase ratios (1920 -> 1280), Lanczos
+// upscaling and degrees 1-9, non-integer Area, Linear at ratios other than 2x.  A workgroup
+// computes a tile of TH output rows x CT output columns of one frame, in two passes through LDS:
+//   1. vertical: the work rows of the tile's source-column span [lo8, lo8 + 8*groups), one task
+//      = (output row, 8 source columns): nYp taps, each an 8-byte buffer load of a clamped row,
+//      a v_perm unpack into u16 pairs (per-lane selectors replicate edge columns) and
+//      v_pk_mad_u16 -- whose low 16 bits are the reference's int16 / u16 wrap;
+//   2. horizontal: a thread owns 4 adjacent output columns (their coefficient pairs live in
+//      VGPRs for the whole tile) and walks the tile's rows: NP v_dot2 over aligned u16 pairs of
+//      the work row, the rounding shift (or the exact border division), one dword store.
+// The per-row / per-column windows come from build_tile_tables (plan.cpp), which folds the
+// reference's identity, replicated-border and masked-border cases into plain tap windows; the
+// results are bit-exact with general_kernel / the reference for every shape.
 
 struct TileArgs {
-    GeneralDev g;
+    TileDev t;
     Io io;
-    int rowBegin, rowEnd, rowsPerBand;
-    int Rmask, pitch;   // ring rows - 1 (a power of two), bytes per ring row
-    int srcBytes;       // buffer range of one frame's source window
-    int maxTaps;        // capacity of the per-thread X coefficient array (>= nX)
+    int rowBegin, rowEnd;
+    int srcBytes, dstBytes;
 };
 
-// A record every lane reads at the same (uniform) address, made provably wave-uniform so that
-// everything derived from it lives in SGPRs and branches on it are scalar.
-__device__ __forceinline__ int4 uniform4(int4 v)
+template <int NP, bool LZ>
+__global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
 {
-    return make_int4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
-                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
-}
-
-// Source rows [a, b) that output row record yi reads (plan.cpp band_src_rows, per row).
-__device__ __forceinline__ void tile_row_window(const GeneralDev &g, int4 yi, int &a, int &b)
-{
-    if (yi.z == KID) {
-        a = yi.x;
-        b = yi.x + 1;
-    } else if (g.method == 2 && yi.z != KMAIN) {
-        a = yi.z == KLO ? 0 : g.srcH - 1;
-        b = a + 1;
-    } else {
-        a = yi.x;
-        b = yi.x + g.nY;
-    }
-    a = max(0, min(a, g.srcH - 1));
-    b = max(a + 1, min(b, g.srcH));
-}
-
-template <int VEC, int CP>
-__global__ __launch_bounds__(256) void tile_kernel(TileArgs t)
-{
-    // CP: work columns per thread, the chunk span rounded up (<= 256 * CP); extra columns are
-    // computed on clamped offsets and dropped.  The ring has a power-of-two row count (mask).
-    extern __shared__ __attribute__((aligned(16))) int tile_lds[];
-    const GeneralDev &g = t.g;
+    extern __shared__ __attribute__((aligned(16))) uint32_t tile_lds[];
+    const TileDev &t = a.t;
     const int tid = static_cast<int>(threadIdx.x);
-    const int chunk = static_cast<int>(blockIdx.x) % g.nChunks;
-    const int band = static_cast<int>(blockIdx.x) / g.nChunks;
-    const int y0 = t.rowBegin + band * t.rowsPerBand;
-    const int y1 = min(y0 + t.rowsPerBand, t.rowEnd);
-    if (y0 >= y1)
-        return;
-    const int4 ch = uniform4(g.chunks[chunk]);  // outputs [xs, xe), source span [lo, hi)
-    const int lo = ch.z, hi = ch.w;
-    const int base = VEC == 16 ? (lo & ~15) : lo;  // first column held by a ring row
-    const int nbytes = hi - base;
-    const int fullBytes = min(nbytes, (g.srcW - base) & ~15);
-    // LDS: work row [ldsInts] | X coefficients [nX][256] (this thread's taps) | ring
-    int *work = tile_lds;
-    int *xc = tile_lds + g.ldsInts;
-    uint8_t *ring = reinterpret_cast<uint8_t *>(xc + t.maxTaps * 256);
+    const int tileX = static_cast<int>(blockIdx.x);
+    const int y0 = a.rowBegin + static_cast<int>(blockIdx.y) * t.TH;
+    const int nRows = min(t.TH, a.rowEnd - y0);
+    uint32_t *const work = tile_lds;
+    int4 *const recs = reinterpret_cast<int4 *>(tile_lds + t.TH * t.pitchDw);
+    uint32_t *const rc = reinterpret_cast<uint32_t *>(recs + t.TH);
 
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.z) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.z) * a.io.dstFrameSt;
+    // alignment of this frame (frame strides may be odd): the source buffer starts at the dword
+    // below the frame; rows are fetched as 8 bytes when base and stride are dword-aligned, else
+    // as 12 dword-aligned bytes and a byte shift.  Stores are dwords only when aligned.
+    const int srcMis = static_cast<int>(reinterpret_cast<uintptr_t>(srcFrame) & 3);
+    const bool srcA4 = srcMis == 0 && !(a.io.srcSt & 3);
+    const bool dstA4 = !(reinterpret_cast<uintptr_t>(dstFrame) & 3) && !(a.io.dstSt & 3);
     const __amdgpu_buffer_rsrc_t srcR = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(t.io.src + static_cast<int64_t>(blockIdx.y) * t.io.srcFrameSt), 0, t.srcBytes, 0x00020000);
-    uint8_t *dstF = t.io.dst + static_cast<int64_t>(blockIdx.y) * t.io.dstFrameSt;
-    const int srcSt = static_cast<int>(t.io.srcSt);
+        const_cast<uint8_t *>(srcFrame - srcMis), 0, a.srcBytes + srcMis, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
 
-    // this thread's output column, its record and its X coefficients (loop-invariant)
-    const int x = ch.x + tid;
-    const bool hasX = x < ch.y;
-    const int4 xi = hasX ? g.xInfo[x] : make_int4(0, 0, KID, 1);
-    const int nX = g.method == 2 ? 2 : g.nX;
-    for (int i = 0; i < nX; ++i)
-        xc[i * 256 + tid] = (hasX && xi.z != KID) ? g.tabX[xi.y + i] : 0;
-    // work columns of this thread: lo + tid + 256 k for k < kmax (ring offsets clamped into the span)
-    int colOff[CP];
+    // this tile's row records and Y coefficients -> LDS
+    for (int i = tid; i < nRows; i += 256)
+        recs[i] = t.rows[y0 + i];
+    for (int i = tid; i < nRows * t.nYp; i += 256)
+        rc[i] = t.rowCoef[static_cast<int64_t>(y0) * t.nYp + i];
+
+    // horizontal ownership: 4 adjacent output columns per thread, rows jStart, jStart + jStep, ...
+    const int nQ = t.CT >> 2;
+    const int q = tid & (nQ - 1), jStart = tid >> t.log2nQ, jStep = 256 >> t.log2nQ;
+    const int x0 = tileX * t.CT + 4 * q;
+    const int4 sp = t.spans[tileX];  // {lo8, groups}
+    uint32_t cf[4][NP];
+    int woff[4], D[4];
 #pragma unroll
-    for (int k = 0; k < CP; ++k)
-        colOff[k] = min(lo + tid + 256 * k, hi - 1) - base;
-    auto W = [&](int col) { return work[max(0, min(col, hi - 1) - lo)]; };
+    for (int k = 0; k < 4; ++k) {
+        const bool in = x0 + k < t.dstW;
+        const int2 col = in ? t.cols[x0 + k] : make_int2(sp.x, 0);
+        woff[k] = (col.x - sp.x) >> 1;
+        D[k] = col.y;
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+            cf[k][p] = in ? t.colCoef[static_cast<int64_t>(x0 + k) * NP + p] : 0u;
+    }
+    __syncthreads();
 
-    // Source rows reach the ring one output row ahead: the rows that enter the window of row y+1
-    // (at most kTileAdv) are loaded into registers while row y is computed, and written to the
-    // ring at the start of row y+1.  The first row of the band loads its window directly.
-    // 16-B aligned layouts only (VEC == 16); the byte path loads each row when it is needed.
-    auto load_row_now = [&](int r) {
-        uint8_t *dr = ring + (r & t.Rmask) * t.pitch;
-        const int so = (r - t.io.srcRow0) * srcSt + base;
-        if constexpr (VEC == 16) {
-            // whole 16-B blocks inside the row (a block crossing the end of the frame's last
-            // row would be out of range as a whole and read as zeros), then the tail bytes
-            for (int off = tid * 16; off < fullBytes; off += 256 * 16) {
-                u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srcR, off, so, 0);
-                *reinterpret_cast<u32x4 *>(dr + off) = v;
+    // 1. vertical pass: tasks (row j, group g), g fastest
+    {
+        const int nG = sp.y;
+        const int dj = 256 / nG, dg = 256 - dj * nG;
+        int j = tid / nG, g = tid - (tid / nG) * nG;
+        const int srcW = t.srcW, srcSt = static_cast<int>(a.io.srcSt), srcRow0 = a.io.srcRow0;
+        const int fmis = srcMis;
+        while (j < nRows) {
+            const int cb = sp.x + 8 * g;
+            const int cbc = max(cb, 0);
+            // last groups of a row: clamped single bytes (a 12-byte window would pass the end of
+            // the frame's last row)
+            const bool edgeR = cb + 12 > srcW;
+            uint32_t s0 = 0x0c010c00u, s1 = 0x0c030c02u, s2 = 0x0c050c04u, s3 = 0x0c070c06u;
+            if (cb < 0 && !edgeR) {  // left edge group: replicate source column 0
+                auto b = [&](int k) { return static_cast<uint32_t>(max(cb + k, 0)); };
+                s0 = b(0) | (b(1) << 16) | 0x0c000c00u;
+                s1 = b(2) | (b(3) << 16) | 0x0c000c00u;
+                s2 = b(4) | (b(5) << 16) | 0x0c000c00u;
+                s3 = b(6) | (b(7) << 16) | 0x0c000c00u;
             }
-            for (int off = fullBytes + tid; off < nbytes; off += 256)
-                dr[off] = __builtin_amdgcn_raw_buffer_load_b8(srcR, off, so, 0);
-        } else {
-            for (int off = tid; off < nbytes; off += 256)
-                dr[off] = __builtin_amdgcn_raw_buffer_load_b8(srcR, off, so, 0);
-        }
-    };
-    u32x4 pf[kTileAdv];  // prefetched 16-B block of row (have1 + j) for this thread
-    uint32_t pfb[kTileAdv];  // ... and one tail byte
-    int nPf = 0;  // rows in the prefetch registers (uniform)
-    const int blk = tid * 16, tailOff = fullBytes + tid;
-    int have1 = INT_MIN;  // source rows [window start, have1) are resident
-    for (int y = y0; y < y1; ++y) {
-        const int4 yi = uniform4(g.yInfo[y]);
-        int ra, rb;
-        tile_row_window(g, yi, ra, rb);
-        if (VEC == 16 && y > y0) {
-            // the rows prefetched during the previous output row ([have1, have1 + nPf) == [.., rb))
+            const int4 r = recs[j];
+            const uint32_t *cj = rc + j * t.nYp;
+            uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
+            for (int i = 0; i < t.nYp; i += 4) {
+                const uint4 c4 = *reinterpret_cast<const uint4 *>(cj + i);
+                u32x2 v[4];
 #pragma unroll
-            for (int j = 0; j < kTileAdv; ++j)
-                if (j < nPf) {
-                    uint8_t *dr = ring + ((have1 + j) & t.Rmask) * t.pitch;
-                    if (blk < fullBytes)
-                        *reinterpret_cast<u32x4 *>(dr + blk) = pf[j];
-                    if (tailOff < nbytes)
-                        dr[tailOff] = static_cast<uint8_t>(pfb[j]);
-                }
-            // rows beyond the prefetch depth (steep downscales) come in now
-            for (int r = max(ra, have1 + kTileAdv); r < rb; ++r)
-                load_row_now(r);
-        } else {
-            for (int r = max(ra, have1); r < rb; ++r)
-                load_row_now(r);
-        }
-        have1 = rb;
-        if (VEC == 16 && y + 1 < y1) {
-            // prefetch the rows entering the next output row's window
-            const int4 yn = uniform4(g.yInfo[y + 1]);
-            int rn0, rn1;
-            tile_row_window(g, yn, rn0, rn1);
-            nPf = min(kTileAdv, max(0, rn1 - max(rb, rn0)));
-            const int r0 = max(rb, rn0);
-            if (rn0 > rb)
-                have1 = INT_MIN;  // the next window jumps past this one: nothing carries over
+                for (int u = 0; u < 4; ++u) {
+                    const int row = min(max(r.x + i + u, r.y), r.z) - srcRow0;
+                    const int o = static_cast<int>(__umul24(row, srcSt)) + fmis;
+                    if (edgeR) {
+                        uint32_t w0 = 0, w1 = 0;
 #pragma unroll
-            for (int j = 0; j < kTileAdv; ++j)
-                if (j < nPf) {
-                    const int so = (r0 + j - t.io.srcRow0) * srcSt + base;
-                    if (blk < fullBytes)
-                        pf[j] = __builtin_amdgcn_raw_buffer_load_b128(srcR, blk, so, 0);
-                    if (tailOff < nbytes)
-                        pfb[j] = __builtin_amdgcn_raw_buffer_load_b8(srcR, tailOff, so, 0);
-                }
-            if (rn0 > rb)
-                have1 = r0;  // written at the next row's start as rows [r0, r0 + nPf)
-        }
-        __syncthreads();  // ring rows visible; the previous row's outputs are done
-
-        // vertical (general_kernel y_value): int32 sums, truncated to the reference's int16 / u16
-        // work type at the end (wrapping sums are exact mod 2^16).  Taps are uniform: row, ring
-        // slot and coefficient come from scalar registers; rows outside the image weigh 0.
-        int acc[CP];
-#pragma unroll
-        for (int k = 0; k < CP; ++k)
-            acc[k] = 0;
-        if (yi.z == KID || (g.method == 2 && yi.z != KMAIN)) {
-            // identity rows / Linear replicated border rows: the single window row times B
-            const int so = (ra & t.Rmask) * t.pitch;
-#pragma unroll
-            for (int k = 0; k < CP; ++k)
-                acc[k] = ring[so + colOff[k]] * (g.method == 0 ? 64 : 256);
-        } else {
-            const int nT = g.method == 2 ? 2 : g.nY;
-            for (int i = 0; i < nT; ++i) {
-                int r = yi.x + i;
-                if (g.method == 2)
-                    r = max(0, min(r, g.srcH - 1));  // Linear main: rows clamp(o), clamp(o + 1)
-                else if (g.method == 1)
-                    r = min(r, g.srcH - 1);  // Area: weight-0 tap past the end clamped
-                const bool in = r >= 0 && r < g.srcH;
-                const int c = in ? __builtin_amdgcn_readfirstlane(g.tabY[yi.y + i]) : 0;
-                const int so = (in ? r & t.Rmask : 0) * t.pitch;
-#pragma unroll
-                for (int k = 0; k < CP; ++k)
-                    acc[k] += ring[so + colOff[k]] * c;
-            }
-        }
-        const bool border = g.method == 0 && yi.z != KMAIN && yi.z != KID;
-#pragma unroll
-        for (int k = 0; k < CP; ++k) {
-            const int col = lo + tid + 256 * k;
-            if (col < hi) {
-                int v;
-                if (g.method == 0) {
-                    v = static_cast<int16_t>(acc[k]);  // resizeYmain :509-515 (int16 wrap)
-                    if (border)  // resizeYborder :477-489
-                        v = static_cast<int16_t>(exact_div(v * 64, yi.w));
-                } else {
-                    v = static_cast<uint16_t>(acc[k]);
-                }
-                work[col - lo] = v;
-            }
-        }
-        __syncthreads();
-
-        // horizontal (general_kernel x_value), coefficients from LDS
-        if (hasX) {
-            int out;
-            if (g.method == 0) {
-                if (xi.z == KID) {
-                    out = clamp255(static_cast<int16_t>((W(xi.x) + 32) >> 6));
-                } else if (xi.z == KMAIN) {
-                    int sum = 0;  // resizeXmain :605-610
-                    for (int i = 0; i < nX; ++i)
-                        sum += W(xi.x + i) * xc[i * 256 + tid];
-                    out = clamp255(static_cast<int16_t>((sum + (1 << 19)) >> 20));
-                } else {
-                    int nume = 0;  // resizeXborder :563-572
-                    for (int i = 0; i < nX; ++i) {
-                        const int col = xi.x + i;
-                        if (col >= 0 && col < g.srcW)
-                            nume += W(col) * xc[i * 256 + tid];
+                        for (int k = 0; k < 8; ++k) {
+                            const uint32_t bt = __builtin_amdgcn_raw_buffer_load_b8(srcR, o + min(max(cb + k, 0), srcW - 1), 0, 0);
+                            if (k < 4)
+                                w0 |= bt << (8 * k);
+                            else
+                                w1 |= bt << (8 * (k - 4));
+                        }
+                        v[u] = u32x2{w0, w1};
+                    } else if (srcA4) {
+                        v[u] = __builtin_amdgcn_raw_buffer_load_b64(srcR, o + cbc, 0, 0);
+                    } else {  // byte-aligned rows: 12 dword-aligned bytes, then a byte shift
+                        const int O = o + cbc, d = O & 3;
+                        const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(srcR, O - d, 0, 0);
+                        v[u] = u32x2{__builtin_amdgcn_alignbyte(w.y, w.x, d), __builtin_amdgcn_alignbyte(w.z, w.y, d)};
                     }
-                    out = clamp255(static_cast<int16_t>(exact_div(nume + (1 << 19), xi.w * 64)));
                 }
-            } else {
-                auto u16clamp = [](int v) {  // uint8(clamp<uint16_t>(0, 255, int16(v)))
-                    uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(v));
-                    return static_cast<int>(u > 255 ? 255 : u);
-                };
-                if (xi.z == KID) {
-                    out = clamp255(static_cast<int16_t>((W(xi.x) + 128) >> 8));
-                } else if (g.method == 1) {  // Area resizeXmain :349-367
-                    int sum = 0;
-                    for (int i = 0; i < nX; ++i)
-                        sum += W(min(xi.x + i, g.srcW - 1)) * xc[i * 256 + tid];
-                    out = u16clamp((sum + (1 << 22)) >> 23);
-                } else if (xi.z == KLO) {  // Linear resizeXborder :355-366
-                    out = u16clamp((W(0) + 128) >> 8);
-                } else if (xi.z == KHI) {
-                    out = u16clamp((W(g.srcW - 1) + 128) >> 8);
-                } else {
-                    const int c0 = max(0, min(xi.x, g.srcW - 1)), c1 = max(0, min(xi.x + 1, g.srcW - 1));
-                    out = u16clamp((W(c0) * xc[tid] + W(c1) * xc[256 + tid] + (1 << 22)) >> 23);  // :400-405
+                const uint32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc0 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s0), cc[u], acc0);
+                    acc1 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s1), cc[u], acc1);
+                    acc2 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s2), cc[u], acc2);
+                    acc3 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s3), cc[u], acc3);
                 }
             }
-            dstF[static_cast<int64_t>(y - t.io.dstRow0) * t.io.dstSt + x] = static_cast<uint8_t>(out);
+            if (LZ && r.w != 0) {  // masked + renormalised border row: int16(nume * 64 / deno)
+                auto dv = [&](uint32_t pr) {
+                    const int lo = exact_div(static_cast<int>(static_cast<int16_t>(pr & 0xffffu)) * 64, r.w);
+                    const int hi = exact_div(static_cast<int>(static_cast<int16_t>(pr >> 16)) * 64, r.w);
+                    return (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
+                };
+                acc0 = dv(acc0);
+                acc1 = dv(acc1);
+                acc2 = dv(acc2);
+                acc3 = dv(acc3);
+            }
+            *reinterpret_cast<uint4 *>(work + j * t.pitchDw + 4 * g) = make_uint4(acc0, acc1, acc2, acc3);
+            j += dj;
+            g += dg;
+            if (g >= nG) {
+                g -= nG;
+                ++j;
+            }
         }
-        // the next row's loads touch only ring rows this row no longer reads (capacity R >= the
-        // largest window); the barrier after them orders the work-row rewrite
+    }
+    __syncthreads();
+
+    // 2. horizontal pass
+    const int dstSt = static_cast<int>(a.io.dstSt);
+    for (int j = jStart; j < nRows; j += jStep) {
+        const uint32_t *w = work + j * t.pitchDw;
+        uint32_t bytes[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int s = LZ ? (1 << 19) : (1 << 22);
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                s = LZ ? sdot2(w[woff[k] + p], cf[k][p], s)
+                       : static_cast<int>(udot2(w[woff[k] + p], cf[k][p], static_cast<uint32_t>(s)));
+            if (LZ) {
+                int v = s >> 20;
+                if (D[k] != 0)
+                    v = exact_div(s, D[k]);
+                bytes[k] = static_cast<uint32_t>(clamp255(static_cast<int16_t>(v)));
+            } else {
+                bytes[k] = min((static_cast<uint32_t>(s) >> 23) & 0xffffu, 255u);
+            }
+        }
+        const int off = (y0 + j - a.io.dstRow0) * dstSt + x0;
+        if (dstA4 && x0 + 4 <= t.dstW) {
+            const uint32_t o = opaque(bytes[0] | (bytes[1] << 8)) | (bytes[2] << 16) | (bytes[3] << 24);
+            __builtin_amdgcn_raw_buffer_store_b32(o, dstR, off, 0, 0);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x0 + k < t.dstW)
+                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(bytes[k]), dstR, off + k, 0, 0);
+        }
     }
 }
 
@@ -2027,35 +1958,43 @@ hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int r
     return hipGetLastError();
 }
 
-hipError_t launch_tile(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, int R, int pitch, int maxTaps,
-                       int cp, bool vec16, hipStream_t s)
+hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd, hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
     const int rows = rowEnd - rowBegin;
-    const int64_t sb = static_cast<int64_t>(g.srcH - io.srcRow0 - 1) * io.srcSt + g.srcW;
-    if (sb >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 31))
+    const int64_t sb = static_cast<int64_t>(t.srcH - io.srcRow0 - 1) * io.srcSt + t.srcW;
+    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + t.dstW;
+    if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24) ||
+        io.dstSt >= (int64_t(1) << 31) || t.srcH >= (1 << 24))
         return hipErrorInvalidValue;
-    const size_t lds = static_cast<size_t>(g.ldsInts + 256 * maxTaps) * sizeof(int) + static_cast<size_t>(R) * pitch;
-    // bands: enough workgroups for ~8 per CU over the batch, at least 8 rows per band (each band
-    // start re-reads its window)
-    const int64_t perBand = static_cast<int64_t>(g.nChunks) * io.frames;
-    int bands = static_cast<int>(std::max<int64_t>(1, (2048 + perBand - 1) / perBand));
-    bands = std::max(1, std::min(bands, rows / 8 > 0 ? rows / 8 : 1));
-    const int rpb = (rows + bands - 1) / bands;
-    bands = (rows + rpb - 1) / rpb;
-    TileArgs t{g, io, rowBegin, rowEnd, rpb, R - 1, pitch, static_cast<int>(sb), maxTaps};
-    dim3 grid(static_cast<unsigned>(bands * g.nChunks), static_cast<unsigned>(io.frames));
-    void *args[] = {&t};
-    const int span = cp;  // 1, 2, 4 or 8 columns per thread
+    TileArgs a{t, io, rowBegin, rowEnd, static_cast<int>(sb), static_cast<int>(db)};
+    const size_t lds = static_cast<size_t>(t.TH) * (static_cast<size_t>(t.pitchDw) * 4 + 16 + static_cast<size_t>(t.nYp) * 4);
+    dim3 grid(static_cast<unsigned>((t.dstW + t.CT - 1) / t.CT), static_cast<unsigned>((rows + t.TH - 1) / t.TH),
+              static_cast<unsigned>(io.frames));
+#define IQO_TILE(NP_)                                                                                \
+    case NP_:                                                                                        \
+        kern = t.lanczos ? reinterpret_cast<const void *>(tile_kernel<NP_, true>)                    \
+                         : reinterpret_cast<const void *>(tile_kernel<NP_, false>);                  \
+        break;
     const void *kern = nullptr;
-#define IQO_TILE(V)                                                                                     \
-    (span <= 1 ? reinterpret_cast<const void *>(tile_kernel<V, 1>)                                     \
-               : span <= 2 ? reinterpret_cast<const void *>(tile_kernel<V, 2>)                         \
-                           : span <= 4 ? reinterpret_cast<const void *>(tile_kernel<V, 4>)             \
-                                       : reinterpret_cast<const void *>(tile_kernel<V, 8>))
-    kern = vec16 ? IQO_TILE(16) : IQO_TILE(1);
+    switch (t.NP) {
+        IQO_TILE(1)
+        IQO_TILE(2)
+        IQO_TILE(3)
+        IQO_TILE(4)
+        IQO_TILE(5)
+        IQO_TILE(6)
+        IQO_TILE(7)
+        IQO_TILE(8)
+        IQO_TILE(10)
+        IQO_TILE(12)
+        IQO_TILE(16)
+    default:
+        return hipErrorInvalidValue;
+    }
 #undef IQO_TILE
+    void *args[] = {&a};
     return hipLaunchKernel(kern, grid, dim3(256), args, lds, s);
 }
 

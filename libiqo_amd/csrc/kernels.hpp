@@ -29,11 +29,18 @@ struct GeneralDev {
     int ldsInts;                 // work-row capacity (ints) of the largest chunk
 };
 hipError_t launch_general(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
-// --- tiled general streamer: same semantics, a workgroup walks a band of rows of one chunk with
-// the source rows in an LDS ring of R rows x pitch bytes (R a power of two >= the largest per-row
-// window); cp = work columns per thread (1, 2, 4, 8: the largest chunk span / 256, rounded up).
-hipError_t launch_tile(const GeneralDev &g, const Io &io, int rowBegin, int rowEnd, int R, int pitch, int maxTaps,
-                       int cp, bool vec16, hipStream_t s);
+// --- separable tile kernel (general ratios): tables from plan.cpp build_tile_tables.
+struct TileDev {
+    bool lanczos;                // int16 work + signed dots (else u16 work, Area / Linear)
+    int srcW, srcH, dstW;
+    int NP, nYp, CT, TH, pitchDw, log2nQ;
+    const int4 *rows;            // TileRec {start, lo, hi, deno} per output row
+    const uint32_t *rowCoef;     // dstH x nYp (c, c) splats
+    const int2 *cols;            // TileCol {a, D} per output column
+    const uint32_t *colCoef;     // dstW x NP pairs
+    const int4 *spans;           // {lo8, groups, 0, 0} per column tile
+};
+hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
 
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {

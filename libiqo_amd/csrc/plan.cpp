@@ -662,6 +662,142 @@ bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW
     return true;
 }
 
+namespace {
+
+// One axis coordinate as a contiguous tap window: source index of tap 0, coefficients (16-bit
+// patterns) and the Lanczos border divisor (0 for every other formula).  Follows y_value /
+// x_value_rec of kernels.hip (and through them the reference lines cited there).
+struct Window {
+    int start = 0;
+    std::vector<int32_t> c;
+    int32_t div = 0;
+    bool border = false;
+};
+
+Window axis_window(const Plan &p, const AxisPlan &ax, int i, bool isX)
+{
+    const CoordInfo &ci = ax.coord[static_cast<size_t>(i)];
+    const int len = ax.srcLen;
+    Window w;
+    w.start = ci.srcO;
+    if (ci.kind == kIdentity) {
+        w.c.assign(1, p.method == kLanczos ? (isX ? 1 << 14 : 64) : (isX ? 1 << 15 : 256));
+        return w;
+    }
+    if (p.method == kLinear && ci.kind != kMain) {  // replicate the first / last source pixel
+        w.start = ci.kind == kBorderLo ? 0 : len - 1;
+        w.c.assign(1, isX ? 1 << 15 : 256);
+        return w;
+    }
+    w.c.assign(ax.table.begin() + ci.tabOff, ax.table.begin() + ci.tabOff + ax.taps);
+    if (p.method == kLanczos && ci.kind != kMain) {
+        for (int k = 0; k < ax.taps; ++k)
+            if (w.start + k < 0 || w.start + k >= len)
+                w.c[static_cast<size_t>(k)] = 0;
+        w.border = true;
+        w.div = isX ? ci.aux * 64 : ci.aux;
+    }
+    return w;
+}
+
+} // namespace
+
+void build_tile_tables(const Plan &p, TileTables *t)
+{
+    *t = TileTables();
+    if (p.srcW < 8)
+        return;
+    // rows
+    int nY = 1;
+    std::vector<Window> wy(static_cast<size_t>(p.dstH));
+    for (int y = 0; y < p.dstH; ++y) {
+        wy[static_cast<size_t>(y)] = axis_window(p, p.y, y, false);
+        nY = std::max(nY, static_cast<int>(wy[static_cast<size_t>(y)].c.size()));
+    }
+    t->nYp = (nY + 3) & ~3;
+    t->rows.resize(static_cast<size_t>(p.dstH));
+    t->rowCoef.assign(static_cast<size_t>(p.dstH) * t->nYp, 0u);
+    for (int y = 0; y < p.dstH; ++y) {
+        const Window &w = wy[static_cast<size_t>(y)];
+        const int n = static_cast<int>(w.c.size());
+        const int lo = std::max(0, std::min(w.start, p.srcH - 1));
+        const int hi = std::max(lo, std::min(w.start + n - 1, p.srcH - 1));
+        // a masked border divisor of 0 traps in the reference; exact_div(n, INT_MAX) = 0 here, as
+        // in general_kernel
+        const int32_t deno = w.border ? (w.div ? w.div : 0x7fffffff) : 0;
+        t->rows[static_cast<size_t>(y)] = TileRec{w.start, lo, hi, deno};
+        for (int k = 0; k < n; ++k) {
+            const uint32_t c = static_cast<uint32_t>(w.c[static_cast<size_t>(k)]) & 0xffffu;
+            t->rowCoef[static_cast<size_t>(y) * t->nYp + k] = c | (c << 16);
+        }
+    }
+    // columns
+    std::vector<Window> wx(static_cast<size_t>(p.dstW));
+    int np = 1;
+    for (int x = 0; x < p.dstW; ++x) {
+        Window &w = wx[static_cast<size_t>(x)];
+        w = axis_window(p, p.x, x, true);
+        const int shift = w.start & 1;
+        np = std::max(np, (static_cast<int>(w.c.size()) + shift + 1) / 2);
+    }
+    int NP = 0;
+    for (int v : kTileNP)
+        if (v >= np) {
+            NP = v;
+            break;
+        }
+    if (!NP)
+        return;  // wider than the largest instantiation: general_kernel
+    t->NP = NP;
+    t->cols.resize(static_cast<size_t>(p.dstW));
+    t->colCoef.assign(static_cast<size_t>(p.dstW) * NP, 0u);
+    for (int x = 0; x < p.dstW; ++x) {
+        const Window &w = wx[static_cast<size_t>(x)];
+        const int a = w.start & ~1, shift = w.start - a;
+        const int32_t D = w.border ? (w.div ? w.div : 0x7fffffff) : 0;
+        t->cols[static_cast<size_t>(x)] = TileCol{a, D};
+        for (int k = 0; k < static_cast<int>(w.c.size()); ++k) {
+            const int slot = k + shift;
+            const uint32_t c = static_cast<uint32_t>(w.c[static_cast<size_t>(k)]) & 0xffffu;
+            t->colCoef[static_cast<size_t>(x) * NP + slot / 2] |= (slot & 1) ? c << 16 : c;
+        }
+    }
+    // column tiles: wider tiles for upscales, so the vertical pass has enough columns per tile
+    const double ratio = static_cast<double>(p.srcW) / p.dstW;
+    int CT = ratio >= 1.0 ? 256 : (ratio >= 0.5 ? 512 : 1024);
+    while (CT > 256 && CT / 2 >= p.dstW)
+        CT /= 2;
+    t->CT = CT;
+    const int nT = (p.dstW + CT - 1) / CT;
+    t->spans.resize(static_cast<size_t>(nT));
+    int maxG = 1;
+    for (int k = 0; k < nT; ++k) {
+        int lo = 1 << 30, hi = -(1 << 30);
+        for (int x = k * CT; x < std::min(p.dstW, (k + 1) * CT); ++x) {
+            lo = std::min(lo, t->cols[static_cast<size_t>(x)].a);
+            hi = std::max(hi, t->cols[static_cast<size_t>(x)].a + 2 * NP);
+        }
+        const int lo8 = lo & ~7;
+        const int g = (hi - lo8 + 7) / 8;
+        t->spans[static_cast<size_t>(k)] = TileSpan{lo8, g};
+        maxG = std::max(maxG, g);
+    }
+    t->pitchDw = 4 * maxG;
+    // rows per tile: 16, fewer when the work tile and the staged row coefficients outgrow 48 KiB
+    int TH = 16;
+    auto lds = [&](int th) { return static_cast<size_t>(th) * (t->pitchDw * 4 + t->nYp * 4 + 16); };
+    while (TH > 4 && lds(TH) > 48 * 1024)
+        TH /= 2;
+    if (lds(TH) > 64 * 1024)
+        return;
+    t->TH = TH;
+    int l2 = 0;
+    while ((4 << l2) < CT)
+        ++l2;
+    t->log2nQ = l2;
+    t->ok = true;
+}
+
 void band_src_rows(const Plan &p, int r0, int r1, int *s0, int *s1)
 {
     int lo = p.srcH, hi = 0;

@@ -103,6 +103,43 @@ struct Plan {
     FastLinear fln;
 };
 
+// Tables of the separable tile kernel (kernels.hip tile_kernel): every shape the specialised
+// kernels do not take.  Each output row and column is restated as ONE contiguous tap window
+// (start, coefficients) with the reference's special cases folded in -- identity rows/columns
+// become a single tap (64 / 2^14 for Lanczos Y / X, 256 / 2^15 for Area and Linear, which give
+// the same rounding), Linear's replicated borders a single tap on the first / last source pixel,
+// masked Lanczos border taps a zero coefficient -- so the kernel runs one formula per axis:
+//   vertical:   work = sum_i px(clamp(start + i, lo, hi)) * c_i    (16-bit wrap, v_pk_mad_u16)
+//   horizontal: sum = bias + sum_i work(clamp(a + i)) * pair_i   (v_dot2 over u16 pairs)
+// Horizontal windows start on an even column a (one leading zero coefficient when the true start
+// is odd), so every pair is one aligned dword of the work row.
+struct TileRec {
+    int32_t start, lo, hi, deno;  // row: first tap, clamp bounds, Lanczos border divisor (0 = main)
+};
+struct TileCol {
+    int32_t a, D;                 // column: even window start, Lanczos border divisor * 64 (0 = main)
+};
+struct TileSpan {
+    int32_t lo8, groups;          // column tile: first work column (multiple of 8), 8-column groups
+};
+struct TileTables {
+    bool ok = false;
+    int NP = 0;                   // coefficient pairs per column (instantiated count)
+    int nYp = 0;                  // taps per row, padded to a multiple of 4 (zero coefficients)
+    int CT = 256;                 // output columns per tile (256, 512 or 1024)
+    int TH = 16;                  // output rows per tile
+    int pitchDw = 0;              // LDS work-row pitch (dwords) = 4 * max groups
+    int log2nQ = 6;               // log2(CT / 4): threads per row in the horizontal pass
+    std::vector<TileRec> rows;    // dstH
+    std::vector<uint32_t> rowCoef;// dstH x nYp, (c, c) u16 splats
+    std::vector<TileCol> cols;    // dstW
+    std::vector<uint32_t> colCoef;// dstW x NP, (c_2p, c_2p+1) u16 pairs from the even start
+    std::vector<TileSpan> spans;  // ceil(dstW / CT)
+};
+// Instantiated pair counts of the tile kernel; build_tile_tables rounds NP up to one of these.
+constexpr int kTileNP[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16};
+void build_tile_tables(const Plan &p, TileTables *t);
+
 // Build the full plan.  Returns false (with *err) for invalid arguments.
 bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                 size_t pxScale, Plan *out, std::string *err);

@@ -100,11 +100,13 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 2, 640, 480, 320, 240, 1), "lanczos_stream"),
     (("area", 0, 7680, 4320, 1920, 1080, 1), "area_int"),
     (("linear", 0, 1920, 1080, 3840, 2160, 1), "linear_up2"),
-    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "general"),
-    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "general"),
-    (("area", 0, 1920, 1080, 1280, 720, 1), "general"),
+    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "tile"),          # general ratios: separable tiles
+    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "tile"),
+    (("area", 0, 1920, 1080, 1280, 720, 1), "tile"),
+    (("linear", 0, 1366, 768, 1000, 1000, 1), "tile"),
     (("lanczos", 3, 1920, 1080, 960, 540, 2), "lanczos_stream"),   # pxScale-2 chroma (ring streamer)
-    (("lanczos", 9, 4000, 3000, 97, 61, 1), "general"),
+    (("lanczos", 9, 4000, 3000, 97, 61, 1), "general"),           # 2 x 9 x 41 taps: beyond NP = 16
+    (("lanczos", 3, 7, 100, 3, 50, 1), "general"),                 # narrower than one 8-byte group
 ])
 def test_fast_path_selection(cfg, kernel):
     assert libiqo_amd.host_kernel_for(*cfg) == kernel

@@ -39,20 +39,18 @@ def test_native_library_is_the_gpu_path():
     assert r.describe()["kernel"] == "lanczos_stream"
 
 
-@pytest.mark.parametrize("force_general", [False, True, "tile"])
+@pytest.mark.parametrize("force_general", [False, True])
 def test_golden_vectors_gpu(golden, force_general):
     """Every golden case, via the host-pointer entry point (reference resize() semantics): default
-    kernels, the reference general_kernel, and the opt-in tiled streamer for every shape without a
-    specialised kernel."""
+    kernels (the separable tile kernel for every shape without a specialised one) and the
+    one-row-per-workgroup general_kernel."""
     n = 0
     for c in golden["cases"]:
         sw, sh, dw, dh = c["srcW"], c["srcH"], c["dstW"], c["dstH"]
         if sw * sh > 4_000_000:
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
-        if force_general == "tile":
-            r.set_option("tile", 1)
-        elif force_general:
+        if force_general:
             r.set_option("force_general", 1)
         src = ol.gen(c["gen"], sw, sh, c["seed"])
         out = _run_host(r, src, dw, dh)
@@ -232,20 +230,27 @@ TILE_SHAPES = [
     ("linear", 0, 640, 480, 1000, 700, 1),      # linear, non-2x
     ("lanczos", 3, 64, 48, 640, 480, 1),        # 10x upscale
     ("lanczos", 3, 3840, 2160, 3840, 1080, 1),  # Y only (X identity)
+    ("lanczos", 3, 1366, 768, 1000, 562, 1),    # width not a multiple of 4 (byte-aligned rows)
+    ("area", 0, 1001, 777, 640, 480, 1),
+    ("linear", 0, 1917, 1079, 1280, 720, 1),    # linear downscale
+    ("lanczos", 9, 500, 400, 1200, 900, 1),     # degree 9 upscale
+    ("lanczos", 1, 1920, 1080, 1000, 600, 1),
+    ("lanczos", 3, 1920, 1080, 400, 220, 1),    # 4.8:1, 30 X taps (16 pairs)
+    ("lanczos", 3, 13, 9, 5, 40, 1),            # narrow: every group is an edge group
 ]
 
 
 @pytest.mark.parametrize("cfg", TILE_SHAPES, ids=lambda c: "%s%d_%dx%d_%dx%d" % c[:6])
 def test_tile_streamer_matches_oracle(cfg):
-    """The tiled general streamer (shapes without a specialised kernel) equals the oracle, with the
-    16-B and the byte load paths (aligned and misaligned bases), and equals the reference
-    general_kernel (tile off) on the same batch."""
+    """The separable tile kernel (shapes without a specialised kernel) equals the oracle with
+    aligned and byte-aligned sources and destinations (8-byte, 12-byte-shifted and single-byte
+    loads; dword and byte stores), and equals general_kernel (plan option tile = 0) on the same
+    batch."""
     m, d, sw, sh, dw, dh, px = cfg
     frames = _noise_batch(2, sw, sh, 1100)
     frames[1, :, : sw // 3] = 255
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    r.set_option("tile", 1)  # opt-in (not yet faster than general_kernel)
     assert r.describe()["kernel"] == "tile"
     src = torch.from_numpy(frames).to(DEV)
     out = r.resize_tensor(src).cpu().numpy()
@@ -262,6 +267,7 @@ def test_tile_streamer_matches_oracle(cfg):
     got = dbuf.view(dh, dw + 5)[:, :dw].cpu().numpy()
     assert (got == exp[0]).all(), cfg
     g = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    g.set_option("tile", 0)
     assert g.describe()["kernel"] == "general"
     assert torch.equal(g.resize_tensor(src), r.resize_tensor(src))
 
