@@ -279,8 +279,12 @@ int upload_tile(iqo_hip_plan *h)
         rows[i] = make_int4(t.rows[i].start, t.rows[i].lo, t.rows[i].hi, t.rows[i].deno);
     for (size_t i = 0; i < cols.size(); ++i)
         cols[i] = make_int2(t.cols[i].a, t.cols[i].D);
-    for (size_t i = 0; i < spans.size(); ++i)
-        spans[i] = make_int4(t.spans[i].lo8, t.spans[i].groups, 0, 0);
+    for (size_t i = 0; i < spans.size(); ++i) {
+        int border = 0;  // any column of the tile with a Lanczos border division
+        for (size_t x = i * t.CT; x < std::min(t.cols.size(), (i + 1) * t.CT); ++x)
+            border |= t.cols[x].D != 0;
+        spans[i] = make_int4(t.spans[i].lo8, t.spans[i].groups, border, 0);
+    }
     int rc;
     if ((rc = upload(&h->dTRows, rows.data(), rows.size())) || (rc = upload(&h->dTCols, cols.data(), cols.size())) ||
         (rc = upload(&h->dTSpans, spans.data(), spans.size())) ||
@@ -437,6 +441,8 @@ iqo_amd::TileDev tile_dev(const iqo_hip_plan *h)
     d.TH = t.TH;
     d.pitchDw = t.pitchDw;
     d.log2nQ = t.log2nQ;
+    d.srcRows = t.srcRows;
+    d.spitch = t.spitch;
     d.rows = h->dTRows;
     d.rowCoef = h->dTRowCoef;
     d.cols = h->dTCols;
@@ -639,6 +645,19 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 62)
             return IQO_HIP_EINVAL;
         h->lanes = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "tile_rows")) {  // output rows per tile of the tile kernel (0 = auto)
+        iqo_amd::TileTables t = h->tt;
+        if (!t.ok)
+            return IQO_HIP_EUNSUP;
+        if (value == 0) {
+            iqo_amd::build_tile_tables(h->p, &t);
+        } else if (!iqo_amd::tile_set_rows(h->p, &t, static_cast<int>(value))) {
+            return IQO_HIP_EINVAL;
+        }
+        h->tt.TH = t.TH;
+        h->tt.srcRows = t.srcRows;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "tile")) {  // 0: shapes without a specialised kernel use general_kernel

@@ -276,9 +276,13 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     const int tileX = static_cast<int>(blockIdx.x);
     const int y0 = a.rowBegin + static_cast<int>(blockIdx.y) * t.TH;
     const int nRows = min(t.TH, a.rowEnd - y0);
+    // LDS: work rows [TH][pitchDw] | row records [TH] | tap records [TH][nYp] (coefficient, LDS
+    // offset of the clamped source row) | border divisors [CT] | source tile [srcRows][spitch]
     uint32_t *const work = tile_lds;
     int4 *const recs = reinterpret_cast<int4 *>(tile_lds + t.TH * t.pitchDw);
-    uint32_t *const rc = reinterpret_cast<uint32_t *>(recs + t.TH);
+    uint2 *const taps = reinterpret_cast<uint2 *>(recs + t.TH);
+    int *const DL = reinterpret_cast<int *>(taps + t.TH * t.nYp);
+    uint8_t *const srcL = reinterpret_cast<uint8_t *>(DL + t.CT);
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.z) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.z) * a.io.dstFrameSt;
@@ -291,91 +295,126 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     const __amdgpu_buffer_rsrc_t srcR = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(srcFrame - srcMis), 0, a.srcBytes + srcMis, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcW = t.srcW, srcSt = static_cast<int>(a.io.srcSt), srcRow0 = a.io.srcRow0;
+    const int4 sp = t.spans[tileX];  // {lo8, groups, any border column}
+    const int spitch = t.spitch;
+    const int rmin = t.rows[y0].y;
+    const int nR = t.rows[y0 + nRows - 1].z - rmin + 1;  // row windows are monotone
+    const int colStart = max(sp.x, 0);
 
-    // this tile's row records and Y coefficients -> LDS
+    // 0. stage the tile's source rows [rmin, rmin + nR) x columns [colStart, lo8 + 8 groups):
+    //    one burst of independent 8-byte loads; the last groups of a row (a whole-word load there
+    //    could pass the end of the frame) as clamped single bytes, replicating the last column
+    {
+        const int sG = sp.y - ((colStart - sp.x) >> 3);
+        const int gE = min(max((srcW - 12 - colStart) / 8 + 1, 0), sG);
+        const int total = nR * gE;
+        for (int t0 = tid; t0 < total; t0 += 256 * 8) {
+            u32x2 v[8];
+            int dstOff[8];
+#pragma unroll
+            for (int b = 0; b < 8; ++b) {
+                const int tt = t0 + 256 * b;
+                const bool valid = tt < total;
+                const int rr = valid ? tt / gE : 0, gg = valid ? tt - rr * gE : 0;
+                const int o = static_cast<int>(__umul24(rmin + rr - srcRow0, srcSt)) + srcMis + colStart + 8 * gg;
+                if (srcA4) {
+                    v[b] = __builtin_amdgcn_raw_buffer_load_b64(srcR, valid ? o : 0x7ff00000, 0, 0);
+                } else {
+                    const int d = o & 3;
+                    const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(srcR, valid ? o - d : 0x7ff00000, 0, 0);
+                    v[b] = u32x2{__builtin_amdgcn_alignbyte(w.y, w.x, d), __builtin_amdgcn_alignbyte(w.z, w.y, d)};
+                }
+                dstOff[b] = valid ? rr * spitch + 8 * gg : -1;
+            }
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                if (dstOff[b] >= 0)
+                    *reinterpret_cast<u32x2 *>(srcL + dstOff[b]) = v[b];
+        }
+        const int nEdge = sG - gE;
+        for (int tt = tid; tt < nR * nEdge; tt += 256) {
+            const int rr = tt / nEdge, gg = gE + (tt - (tt / nEdge) * nEdge);
+            const int o = static_cast<int>(__umul24(rmin + rr - srcRow0, srcSt)) + srcMis;
+            const int c = colStart + 8 * gg;
+            uint32_t w0 = 0, w1 = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t bt = __builtin_amdgcn_raw_buffer_load_b8(srcR, o + min(c + k, srcW - 1), 0, 0);
+                if (k < 4)
+                    w0 |= bt << (8 * k);
+                else
+                    w1 |= bt << (8 * (k - 4));
+            }
+            *reinterpret_cast<u32x2 *>(srcL + rr * spitch + 8 * gg) = u32x2{w0, w1};
+        }
+    }
+    // row records, tap records, border divisors
     for (int i = tid; i < nRows; i += 256)
         recs[i] = t.rows[y0 + i];
-    for (int i = tid; i < nRows * t.nYp; i += 256)
-        rc[i] = t.rowCoef[static_cast<int64_t>(y0) * t.nYp + i];
+    for (int i = tid; i < nRows * t.nYp; i += 256) {
+        const int j = i / t.nYp, tap = i - j * t.nYp;
+        const int4 r = t.rows[y0 + j];
+        taps[i] = make_uint2(t.rowCoef[static_cast<int64_t>(y0) * t.nYp + i],
+                             static_cast<uint32_t>((min(max(r.x + tap, r.y), r.z) - rmin) * spitch));
+    }
+    const bool borderTile = LZ && sp.z;
+    if (borderTile)
+        for (int i = tid; i < t.CT; i += 256)
+            DL[i] = tileX * t.CT + i < t.dstW ? t.cols[tileX * t.CT + i].y : 0;
 
     // horizontal ownership: 4 adjacent output columns per thread, rows jStart, jStart + jStep, ...
     const int nQ = t.CT >> 2;
     const int q = tid & (nQ - 1), jStart = tid >> t.log2nQ, jStep = 256 >> t.log2nQ;
     const int x0 = tileX * t.CT + 4 * q;
-    const int4 sp = t.spans[tileX];  // {lo8, groups}
     uint32_t cf[4][NP];
-    int woff[4], D[4];
+    int woff[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const bool in = x0 + k < t.dstW;
         const int2 col = in ? t.cols[x0 + k] : make_int2(sp.x, 0);
         woff[k] = (col.x - sp.x) >> 1;
-        D[k] = col.y;
 #pragma unroll
         for (int p = 0; p < NP; ++p)
             cf[k][p] = in ? t.colCoef[static_cast<int64_t>(x0 + k) * NP + p] : 0u;
     }
     __syncthreads();
 
-    // 1. vertical pass: tasks (row j, group g), g fastest
+    // 1. vertical pass: tasks (row j, group g), g fastest; taps from the staged tile
     {
         const int nG = sp.y;
         const int dj = 256 / nG, dg = 256 - dj * nG;
         int j = tid / nG, g = tid - (tid / nG) * nG;
-        const int srcW = t.srcW, srcSt = static_cast<int>(a.io.srcSt), srcRow0 = a.io.srcRow0;
-        const int fmis = srcMis;
         while (j < nRows) {
             const int cb = sp.x + 8 * g;
-            const int cbc = max(cb, 0);
-            // last groups of a row: clamped single bytes (a 12-byte window would pass the end of
-            // the frame's last row)
-            const bool edgeR = cb + 12 > srcW;
             uint32_t s0 = 0x0c010c00u, s1 = 0x0c030c02u, s2 = 0x0c050c04u, s3 = 0x0c070c06u;
-            if (cb < 0 && !edgeR) {  // left edge group: replicate source column 0
+            if (cb < 0) {  // left edge group: replicate source column 0
                 auto b = [&](int k) { return static_cast<uint32_t>(max(cb + k, 0)); };
                 s0 = b(0) | (b(1) << 16) | 0x0c000c00u;
                 s1 = b(2) | (b(3) << 16) | 0x0c000c00u;
                 s2 = b(4) | (b(5) << 16) | 0x0c000c00u;
                 s3 = b(6) | (b(7) << 16) | 0x0c000c00u;
             }
-            const int4 r = recs[j];
-            const uint32_t *cj = rc + j * t.nYp;
+            const uint8_t *colL = srcL + (max(cb, 0) - colStart);
+            const uint2 *tj = taps + j * t.nYp;
             uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-            for (int i = 0; i < t.nYp; i += 4) {
-                const uint4 c4 = *reinterpret_cast<const uint4 *>(cj + i);
-                u32x2 v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int row = min(max(r.x + i + u, r.y), r.z) - srcRow0;
-                    const int o = static_cast<int>(__umul24(row, srcSt)) + fmis;
-                    if (edgeR) {
-                        uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            const uint32_t bt = __builtin_amdgcn_raw_buffer_load_b8(srcR, o + min(max(cb + k, 0), srcW - 1), 0, 0);
-                            if (k < 4)
-                                w0 |= bt << (8 * k);
-                            else
-                                w1 |= bt << (8 * (k - 4));
-                        }
-                        v[u] = u32x2{w0, w1};
-                    } else if (srcA4) {
-                        v[u] = __builtin_amdgcn_raw_buffer_load_b64(srcR, o + cbc, 0, 0);
-                    } else {  // byte-aligned rows: 12 dword-aligned bytes, then a byte shift
-                        const int O = o + cbc, d = O & 3;
-                        const u32x3 w = __builtin_amdgcn_raw_buffer_load_b96(srcR, O - d, 0, 0);
-                        v[u] = u32x2{__builtin_amdgcn_alignbyte(w.y, w.x, d), __builtin_amdgcn_alignbyte(w.z, w.y, d)};
-                    }
-                }
-                const uint32_t cc[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    acc0 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s0), cc[u], acc0);
-                    acc1 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s1), cc[u], acc1);
-                    acc2 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s2), cc[u], acc2);
-                    acc3 = pk_mad(__builtin_amdgcn_perm(v[u].y, v[u].x, s3), cc[u], acc3);
-                }
+#ifdef IQO_TILE_UNROLL2
+#pragma unroll 2
+#endif
+            for (int i = 0; i < t.nYp; i += 2) {
+                const uint4 c2 = *reinterpret_cast<const uint4 *>(tj + i);  // (coef, offset) x 2
+                const u32x2 v0 = *reinterpret_cast<const u32x2 *>(colL + c2.y);
+                const u32x2 v1 = *reinterpret_cast<const u32x2 *>(colL + c2.w);
+                acc0 = pk_mad(__builtin_amdgcn_perm(v0.y, v0.x, s0), c2.x, acc0);
+                acc1 = pk_mad(__builtin_amdgcn_perm(v0.y, v0.x, s1), c2.x, acc1);
+                acc2 = pk_mad(__builtin_amdgcn_perm(v0.y, v0.x, s2), c2.x, acc2);
+                acc3 = pk_mad(__builtin_amdgcn_perm(v0.y, v0.x, s3), c2.x, acc3);
+                acc0 = pk_mad(__builtin_amdgcn_perm(v1.y, v1.x, s0), c2.z, acc0);
+                acc1 = pk_mad(__builtin_amdgcn_perm(v1.y, v1.x, s1), c2.z, acc1);
+                acc2 = pk_mad(__builtin_amdgcn_perm(v1.y, v1.x, s2), c2.z, acc2);
+                acc3 = pk_mad(__builtin_amdgcn_perm(v1.y, v1.x, s3), c2.z, acc3);
             }
+            const int4 r = recs[j];
             if (LZ && r.w != 0) {  // masked + renormalised border row: int16(nume * 64 / deno)
                 auto dv = [&](uint32_t pr) {
                     const int lo = exact_div(static_cast<int>(static_cast<int16_t>(pr & 0xffffu)) * 64, r.w);
@@ -411,10 +450,13 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
                 s = LZ ? sdot2(w[woff[k] + p], cf[k][p], s)
                        : static_cast<int>(udot2(w[woff[k] + p], cf[k][p], static_cast<uint32_t>(s)));
             if (LZ) {
-                int v = s >> 20;
-                if (D[k] != 0)
-                    v = exact_div(s, D[k]);
-                bytes[k] = static_cast<uint32_t>(clamp255(static_cast<int16_t>(v)));
+                int v = s >> 20;  // within int16: the reference's int16 cast is the identity here
+                if (borderTile) {
+                    const int Dk = DL[4 * q + k];
+                    if (Dk != 0)
+                        v = static_cast<int16_t>(exact_div(s, Dk));
+                }
+                bytes[k] = static_cast<uint32_t>(min(max(v, 0), 255));
             } else {
                 bytes[k] = min((static_cast<uint32_t>(s) >> 23) & 0xffffu, 255u);
             }
@@ -1969,7 +2011,8 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
         io.dstSt >= (int64_t(1) << 31) || t.srcH >= (1 << 24))
         return hipErrorInvalidValue;
     TileArgs a{t, io, rowBegin, rowEnd, static_cast<int>(sb), static_cast<int>(db)};
-    const size_t lds = static_cast<size_t>(t.TH) * (static_cast<size_t>(t.pitchDw) * 4 + 16 + static_cast<size_t>(t.nYp) * 4);
+    const size_t lds = static_cast<size_t>(t.TH) * (static_cast<size_t>(t.pitchDw) * 4 + 16 + static_cast<size_t>(t.nYp) * 8) +
+                       4u * static_cast<size_t>(t.CT) + static_cast<size_t>(t.srcRows) * t.spitch;
     dim3 grid(static_cast<unsigned>((t.dstW + t.CT - 1) / t.CT), static_cast<unsigned>((rows + t.TH - 1) / t.TH),
               static_cast<unsigned>(io.frames));
 #define IQO_TILE(NP_)                                                                                \

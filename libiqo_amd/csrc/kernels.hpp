@@ -34,11 +34,12 @@ struct TileDev {
     bool lanczos;                // int16 work + signed dots (else u16 work, Area / Linear)
     int srcW, srcH, dstW;
     int NP, nYp, CT, TH, pitchDw, log2nQ;
+    int srcRows, spitch;         // staged source tile: rows (max over any TH output rows), pitch
     const int4 *rows;            // TileRec {start, lo, hi, deno} per output row
     const uint32_t *rowCoef;     // dstH x nYp (c, c) splats
     const int2 *cols;            // TileCol {a, D} per output column
     const uint32_t *colCoef;     // dstW x NP pairs
-    const int4 *spans;           // {lo8, groups, 0, 0} per column tile
+    const int4 *spans;           // {lo8, groups, any border column, 0} per column tile
 };
 hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
 

@@ -125,11 +125,13 @@ struct TileSpan {
 struct TileTables {
     bool ok = false;
     int NP = 0;                   // coefficient pairs per column (instantiated count)
-    int nYp = 0;                  // taps per row, padded to a multiple of 4 (zero coefficients)
+    int nYp = 0;                  // taps per row, padded to a multiple of 2 (zero coefficients)
     int CT = 256;                 // output columns per tile (256, 512 or 1024)
     int TH = 16;                  // output rows per tile
     int pitchDw = 0;              // LDS work-row pitch (dwords) = 4 * max groups
     int log2nQ = 6;               // log2(CT / 4): threads per row in the horizontal pass
+    int srcRows = 0;              // source rows staged per tile: max over any TH consecutive rows
+    int spitch = 0;               // staged source row pitch (bytes) = 8 * max groups
     std::vector<TileRec> rows;    // dstH
     std::vector<uint32_t> rowCoef;// dstH x nYp, (c, c) u16 splats
     std::vector<TileCol> cols;    // dstW
@@ -139,6 +141,11 @@ struct TileTables {
 // Instantiated pair counts of the tile kernel; build_tile_tables rounds NP up to one of these.
 constexpr int kTileNP[] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 12, 16};
 void build_tile_tables(const Plan &p, TileTables *t);
+// Rows per tile: LDS bytes of a workgroup, staged source rows, and setting TH (false if the
+// workgroup would need more than 64 KiB of LDS).
+size_t tile_lds_bytes(const Plan &p, const TileTables &t, int TH);
+int tile_src_rows(const Plan &p, const TileTables &t, int TH);
+bool tile_set_rows(const Plan &p, TileTables *t, int TH);
 
 // Build the full plan.  Returns false (with *err) for invalid arguments.
 bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
