@@ -50,11 +50,11 @@ enum { IQO_METHOD_LANCZOS = 0, IQO_METHOD_AREA = 1, IQO_METHOD_LINEAR = 2 };
 
 /* Kernel families a plan can dispatch to (iqo_hip_plan_desc.kernel). */
 enum {
-    IQO_KERNEL_GENERAL = 0,     /* any shape, any layout: one workgroup per output row (reference kernel) */
+    IQO_KERNEL_GENERAL = 0,     /* any shape, any layout: one workgroup per output row (fallback) */
     IQO_KERNEL_LANCZOS_STREAM = 1, /* integer ratio, 1 phase: row-band walker, register window */
     IQO_KERNEL_AREA_INT = 2,    /* integer ratio area */
     IQO_KERNEL_LINEAR_UP2 = 3,  /* exact 2x bilinear upsampling */
-    IQO_KERNEL_TILE = 4         /* any other shape: separable tiles (TH rows x CT columns, work rows in LDS) */
+    IQO_KERNEL_TILE = 4         /* general ratios, any layout: separable tiles (TH rows x CT columns) */
 };
 
 typedef struct iqo_hip_plan iqo_hip_plan;
@@ -81,7 +81,11 @@ void iqo_hip_plan_destroy(iqo_hip_plan *plan);
 
 int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
 
-/* Options (tests / tuning): "force_general" (0/1), "bands" (row bands per frame, 0 = auto). */
+/* Options (tests / tuning): "force_general" (0/1: every shape through IQO_KERNEL_GENERAL),
+ * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
+ * IQO_KERNEL_GENERAL instead of IQO_KERNEL_TILE), "tile_rows" (output rows per tile, 0 = auto),
+ * "prefetch", "lin_prefetch", "stream_variant", "lanes", "chunk_frames", "debug_flags" (A/B
+ * experiments; see libiqo_amd/csrc/abi.hip).  IQO_HIP_EINVAL for an unknown key or value. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);
 
 /* Drop-in resize with HOST pointers (byte strides), synchronous: H2D, kernels, D2H. */
