@@ -45,7 +45,10 @@ struct iqo_hip_plan {
     bool useTile = true;
     int4 *dTRows = nullptr, *dTSpans = nullptr;
     int2 *dTCols = nullptr;
-    uint32_t *dTRowCoef = nullptr, *dTColCoef = nullptr;
+    uint2 *dTRowTap = nullptr;
+    uint32_t *dTColCoef = nullptr;
+    int32_t *dTColA = nullptr;
+    int tileNQp = 0;
 };
 
 namespace {
@@ -254,8 +257,9 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dTRows);
     (void)hipFree(h->dTCols);
     (void)hipFree(h->dTSpans);
-    (void)hipFree(h->dTRowCoef);
+    (void)hipFree(h->dTRowTap);
     (void)hipFree(h->dTColCoef);
+    (void)hipFree(h->dTColA);
     delete h;
 }
 
@@ -285,11 +289,34 @@ int upload_tile(iqo_hip_plan *h)
             border |= t.cols[x].D != 0;
         spans[i] = make_int4(t.spans[i].lo8, t.spans[i].groups, border, 0);
     }
+    // column coefficients transposed to [pair p][column-in-quad k][quad Q] (and window starts to
+    // [k][Q]) over the padded tile width, so that a wave's load of one (p, k) is 64 consecutive
+    // dwords; padding quads get zero coefficients and their tile's start (woff 0)
+    const int nQp = static_cast<int>(spans.size()) * t.CT / 4;
+    std::vector<uint32_t> coefT(static_cast<size_t>(t.NP) * 4 * nQp, 0u);
+    std::vector<int32_t> colA(static_cast<size_t>(4) * nQp, 0);
+    for (int Q = 0; Q < nQp; ++Q)
+        for (int k = 0; k < 4; ++k) {
+            const int x = 4 * Q + k;
+            const bool in = x < static_cast<int>(t.cols.size());
+            colA[static_cast<size_t>(k) * nQp + Q] = in ? t.cols[static_cast<size_t>(x)].a : t.spans[static_cast<size_t>(4 * Q / t.CT)].lo8;
+            for (int p = 0; p < t.NP; ++p)
+                coefT[(static_cast<size_t>(p) * 4 + k) * nQp + Q] = in ? t.colCoef[static_cast<size_t>(x) * t.NP + p] : 0u;
+        }
+    h->tileNQp = nQp;
+    // per (row, tap): coefficient splat and the clamped source row it reads
+    std::vector<uint2> rowTap(t.rowCoef.size());
+    for (size_t y = 0; y < t.rows.size(); ++y)
+        for (int i = 0; i < t.nYp; ++i) {
+            const iqo_amd::TileRec &r = t.rows[y];
+            const int row = std::min(std::max(r.start + i, r.lo), r.hi);
+            rowTap[y * t.nYp + i] = make_uint2(t.rowCoef[y * t.nYp + i], static_cast<uint32_t>(row));
+        }
     int rc;
     if ((rc = upload(&h->dTRows, rows.data(), rows.size())) || (rc = upload(&h->dTCols, cols.data(), cols.size())) ||
         (rc = upload(&h->dTSpans, spans.data(), spans.size())) ||
-        (rc = upload(&h->dTRowCoef, t.rowCoef.data(), t.rowCoef.size())) ||
-        (rc = upload(&h->dTColCoef, t.colCoef.data(), t.colCoef.size())))
+        (rc = upload(&h->dTRowTap, rowTap.data(), rowTap.size())) ||
+        (rc = upload(&h->dTColCoef, coefT.data(), coefT.size())) || (rc = upload(&h->dTColA, colA.data(), colA.size())))
         return rc;
     return IQO_HIP_OK;
 }
@@ -444,9 +471,11 @@ iqo_amd::TileDev tile_dev(const iqo_hip_plan *h)
     d.srcRows = t.srcRows;
     d.spitch = t.spitch;
     d.rows = h->dTRows;
-    d.rowCoef = h->dTRowCoef;
+    d.rowTap = h->dTRowTap;
     d.cols = h->dTCols;
     d.colCoef = h->dTColCoef;
+    d.colA = h->dTColA;
+    d.nQp = h->tileNQp;
     d.spans = h->dTSpans;
     return d;
 }

@@ -307,8 +307,11 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     //    could pass the end of the frame) as clamped single bytes, replicating the last column
     {
         const int sG = sp.y - ((colStart - sp.x) >> 3);
-        const int gE = min(max((srcW - 12 - colStart) / 8 + 1, 0), sG);
+        const int gNum = srcW - 12 - colStart;  // groups with c + 12 <= srcW (floor division)
+        const int gE = gNum < 0 ? 0 : min(gNum / 8 + 1, sG);
         const int total = nR * gE;
+        // n / gE = umulhi(n, mG) (exact for n * gE < 2^32); gE = 1 has no 32-bit magic
+        const uint32_t mG = gE > 1 ? 0xffffffffu / static_cast<uint32_t>(gE) + 1u : 0u;
         for (int t0 = tid; t0 < total; t0 += 256 * 8) {
             u32x2 v[8];
             int dstOff[8];
@@ -316,7 +319,8 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
             for (int b = 0; b < 8; ++b) {
                 const int tt = t0 + 256 * b;
                 const bool valid = tt < total;
-                const int rr = valid ? tt / gE : 0, gg = valid ? tt - rr * gE : 0;
+                const int rr = valid ? (gE > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(tt), mG)) : tt) : 0;
+                const int gg = valid ? tt - rr * gE : 0;
                 const int o = static_cast<int>(__umul24(rmin + rr - srcRow0, srcSt)) + srcMis + colStart + 8 * gg;
                 if (srcA4) {
                     v[b] = __builtin_amdgcn_raw_buffer_load_b64(srcR, valid ? o : 0x7ff00000, 0, 0);
@@ -353,10 +357,8 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     for (int i = tid; i < nRows; i += 256)
         recs[i] = t.rows[y0 + i];
     for (int i = tid; i < nRows * t.nYp; i += 256) {
-        const int j = i / t.nYp, tap = i - j * t.nYp;
-        const int4 r = t.rows[y0 + j];
-        taps[i] = make_uint2(t.rowCoef[static_cast<int64_t>(y0) * t.nYp + i],
-                             static_cast<uint32_t>((min(max(r.x + tap, r.y), r.z) - rmin) * spitch));
+        const uint2 rt = t.rowTap[static_cast<int64_t>(y0) * t.nYp + i];  // (coefficient, clamped row)
+        taps[i] = make_uint2(rt.x, static_cast<uint32_t>((static_cast<int>(rt.y) - rmin) * spitch));
     }
     const bool borderTile = LZ && sp.z;
     if (borderTile)
@@ -369,14 +371,13 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     const int x0 = tileX * t.CT + 4 * q;
     uint32_t cf[4][NP];
     int woff[4];
+    const int Q = x0 >> 2;  // coalesced: lane-consecutive quads
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const bool in = x0 + k < t.dstW;
-        const int2 col = in ? t.cols[x0 + k] : make_int2(sp.x, 0);
-        woff[k] = (col.x - sp.x) >> 1;
+        woff[k] = (t.colA[k * t.nQp + Q] - sp.x) >> 1;
 #pragma unroll
         for (int p = 0; p < NP; ++p)
-            cf[k][p] = in ? t.colCoef[static_cast<int64_t>(x0 + k) * NP + p] : 0u;
+            cf[k][p] = t.colCoef[(p * 4 + k) * t.nQp + Q];
     }
     __syncthreads();
 

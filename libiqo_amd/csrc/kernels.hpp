@@ -36,9 +36,11 @@ struct TileDev {
     int NP, nYp, CT, TH, pitchDw, log2nQ;
     int srcRows, spitch;         // staged source tile: rows (max over any TH output rows), pitch
     const int4 *rows;            // TileRec {start, lo, hi, deno} per output row
-    const uint32_t *rowCoef;     // dstH x nYp (c, c) splats
+    const uint2 *rowTap;         // dstH x nYp {(c, c) splat, clamped source row}
     const int2 *cols;            // TileCol {a, D} per output column
-    const uint32_t *colCoef;     // dstW x NP pairs
+    const uint32_t *colCoef;     // [NP][4][nQp] pairs (pair, column in quad, quad)
+    const int *colA;             // [4][nQp] even window starts
+    int nQp;                     // quads of the padded tile width
     const int4 *spans;           // {lo8, groups, any border column, 0} per column tile
 };
 hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd, hipStream_t s);

@@ -793,11 +793,11 @@ void build_tile_tables(const Plan &p, TileTables *t)
     while ((4 << l2) < CT)
         ++l2;
     t->log2nQ = l2;
-    // rows per tile: 32, fewer when the staged source, the work tile and the tap records outgrow
-    // 64 KiB (measured on MI355X, G1 1080p -> 720p: 8 rows 0.77 ms, 16 rows 0.42 ms, 32 rows
-    // 0.37 ms per 128 frames -- the per-tile load latency dominates, not the occupancy)
-    int TH = 32;
-    while (TH > 2 && tile_lds_bytes(p, *t, TH) > 64 * 1024)
+    // rows per tile: 16, fewer when the staged source, the work tile and the tap records outgrow
+    // 48 KiB (MI355X, G1 1080p -> 720p x128: 16 rows 0.294 ms, 32 rows 0.315 ms; G3 0.154 vs
+    // 0.183 ms)
+    int TH = 16;
+    while (TH > 2 && tile_lds_bytes(p, *t, TH) > 48 * 1024)
         TH /= 2;
     t->ok = tile_set_rows(p, t, TH);
 }
