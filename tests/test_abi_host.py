@@ -110,3 +110,18 @@ def test_host_tables_match_oracle_random():
 ])
 def test_fast_path_selection(cfg, kernel):
     assert libiqo_amd.host_kernel_for(*cfg) == kernel
+
+
+@pytest.mark.parametrize("tool", ["iqo_resize_yuv420p", "iqo_benchmark"])
+def test_cli_tools_usage_without_gpu(tool, tmp_path):
+    """The two command-line tools are built against the library and reject bad arguments with
+    EINVAL and a usage line before touching the device (reference: sample/resize_yuv420p.cpp:48-55,
+    benchmark/benchmark.cpp)."""
+    exe = os.path.join(os.path.dirname(libiqo_amd.LIB_PATH), "build", tool)
+    assert os.access(exe, os.X_OK), exe
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 22 and "usage:" in r.stdout
+    if tool == "iqo_resize_yuv420p":
+        r = subprocess.run([exe, "-m", "lanczos0", "-i", str(tmp_path / "a"), "-o", str(tmp_path / "b"),
+                            "-iw", "4", "-ih", "4", "-ow", "2", "-oh", "2"], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 22 and "invalid method" in r.stdout

@@ -428,3 +428,41 @@ def test_cpp_dropin_benchmark_cli(tmp_path, m, iw, ih, ow, oh):
     degree = int(m[7]) if method == "lanczos" else 0
     exp = ol.run_oracle(method, degree, iw, ih, ow, oh, 1, ol.gen("mt19937", iw, ih))
     assert (got == exp).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,iw,ih,ow,oh", [("lanczos3", 400, 300, 200, 150), ("lanczos", 301, 203, 150, 101),
+                                           ("area", 640, 480, 320, 240), ("linear", 161, 121, 320, 240)])
+def test_sample_yuv420p_file_tool(tmp_path, m, iw, ih, ow, oh):
+    """The raw-I420 file tool (sample/iqo_resize_yuv420p.cpp, the reference's
+    sample/resize_yuv420p.cpp interface): two frames of a file, every plane equal to the Generic
+    oracle on the reference's plane geometry (luma W x H at stride W+W%2, chroma (W+W%2)/2 x
+    (H+H%2)/2, Lanczos chroma at pxScale 2).  Even shapes take the one-plan YUV420 path, odd ones
+    the three drop-in resizer objects."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(libiqo_amd.LIB_PATH), "build", "iqo_resize_yuv420p")
+    sx, sy, dx, dy = iw + iw % 2, ih + ih % 2, ow + ow % 2, oh + oh % 2
+    nsrc, ndst = sx * sy * 3 // 2, dx * dy * 3 // 2
+    raw = np.concatenate([ol.splitmix_bytes(nsrc, 11), ol.splitmix_bytes(nsrc, 12)]).astype(np.uint8)
+    fin, fout = tmp_path / "in.yuv", tmp_path / "out.yuv"
+    raw.tofile(str(fin))
+    r = subprocess.run([exe, "-m", m, "-i", str(fin), "-iw", str(iw), "-ih", str(ih), "-o", str(fout),
+                        "-ow", str(ow), "-oh", str(oh), "-frames", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(str(fout), dtype=np.uint8)
+    assert got.size == 2 * ndst
+    method = "lanczos" if m.startswith("lanczos") else m
+    degree = (int(m[7]) if len(m) == 8 else 2) if method == "lanczos" else 0
+    pxc = 2 if method == "lanczos" else 1
+    for f in range(2):
+        s, d = raw[f * nsrc:(f + 1) * nsrc], got[f * ndst:(f + 1) * ndst]
+        sY, dY = s[:sx * sy].reshape(sy, sx), d[:dx * dy].reshape(dy, dx)
+        exp = ol.run_oracle(method, degree, iw, ih, ow, oh, 1, sY[:ih, :iw])
+        assert (dY[:oh, :ow] == exp).all(), (m, f, "Y")
+        cs, cd = sx * sy // 4, dx * dy // 4
+        for p, name in ((0, "U"), (1, "V")):
+            sc = s[sx * sy + p * cs: sx * sy + (p + 1) * cs].reshape(sy // 2, sx // 2)
+            dc = d[dx * dy + p * cd: dx * dy + (p + 1) * cd].reshape(dy // 2, dx // 2)
+            exp = ol.run_oracle(method, degree, sx // 2, sy // 2, dx // 2, dy // 2, pxc, sc)
+            assert (dc == exp).all(), (m, f, name)
