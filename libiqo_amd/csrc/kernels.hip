@@ -265,7 +265,13 @@ struct TileArgs {
     Io io;
     int rowBegin, rowEnd;
     int srcBytes, dstBytes;
+    int nTx, nTy;       // column tiles, row tiles per frame
+    unsigned nTiles;    // nTx * nTy * frames (flat grid)
 };
+
+#ifndef IQO_TILE_XCD
+#define IQO_TILE_XCD 1  // XCD-aware flat tile order (0: 3-D grid in dispatch order, A/B only)
+#endif
 
 template <int NP, bool LZ>
 __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
@@ -273,8 +279,33 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     extern __shared__ __attribute__((aligned(16))) uint32_t tile_lds[];
     const TileDev &t = a.t;
     const int tid = static_cast<int>(threadIdx.x);
-    const int tileX = static_cast<int>(blockIdx.x);
-    const int y0 = a.rowBegin + static_cast<int>(blockIdx.y) * t.TH;
+#if IQO_TILE_XCD
+    // Workgroups are dispatched round-robin over the 8 XCDs (flat id L goes to XCD L mod 8), and
+    // each XCD has its own L2.  Give XCD x a contiguous range of tiles, row tiles fastest: the
+    // tiles resident on one XCD at a time are vertical (and horizontal) neighbours, so the halo
+    // rows / columns they share are fetched from HBM once and hit that XCD's L2 afterwards.
+    int tileX, tileY, frame;
+    {
+        const unsigned L = blockIdx.x, N = a.nTiles;
+        const unsigned xcd = L & 7u, idx = L >> 3, q = N >> 3, r = N & 7u;
+        const unsigned lg = xcd < r ? xcd * (q + 1u) + idx : r * (q + 1u) + (xcd - r) * q + idx;
+#if IQO_TILE_XCD == 2  // A/B: column tiles fastest
+        const unsigned rest = lg / static_cast<unsigned>(a.nTx);
+        tileX = static_cast<int>(lg - rest * static_cast<unsigned>(a.nTx));
+        frame = static_cast<int>(rest / static_cast<unsigned>(a.nTy));
+        tileY = static_cast<int>(rest - static_cast<unsigned>(frame) * static_cast<unsigned>(a.nTy));
+#else
+        const unsigned rest = lg / static_cast<unsigned>(a.nTy);
+        tileY = static_cast<int>(lg - rest * static_cast<unsigned>(a.nTy));
+        frame = static_cast<int>(rest / static_cast<unsigned>(a.nTx));
+        tileX = static_cast<int>(rest - static_cast<unsigned>(frame) * static_cast<unsigned>(a.nTx));
+#endif
+    }
+#else
+    const int tileX = static_cast<int>(blockIdx.x), tileY = static_cast<int>(blockIdx.y);
+    const int frame = static_cast<int>(blockIdx.z);
+#endif
+    const int y0 = a.rowBegin + tileY * t.TH;
     const int nRows = min(t.TH, a.rowEnd - y0);
     // LDS: work rows [TH][pitchDw] | row records [TH] | tap records [TH][nYp] (coefficient, LDS
     // offset of the clamped source row) | border divisors [CT] | source tile [srcRows][spitch]
@@ -284,8 +315,8 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     int *const DL = reinterpret_cast<int *>(taps + t.TH * t.nYp);
     uint8_t *const srcL = reinterpret_cast<uint8_t *>(DL + t.CT);
 
-    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(blockIdx.z) * a.io.srcFrameSt;
-    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(blockIdx.z) * a.io.dstFrameSt;
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
     // alignment of this frame (frame strides may be odd): the source buffer starts at the dword
     // below the frame; rows are fetched as 8 bytes when base and stride are dword-aligned, else
     // as 12 dword-aligned bytes and a byte shift.  Stores are dwords only when aligned.
@@ -2011,11 +2042,19 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24) ||
         io.dstSt >= (int64_t(1) << 31) || t.srcH >= (1 << 24))
         return hipErrorInvalidValue;
-    TileArgs a{t, io, rowBegin, rowEnd, static_cast<int>(sb), static_cast<int>(db)};
+    const int nTx = (t.dstW + t.CT - 1) / t.CT, nTy = (rows + t.TH - 1) / t.TH;
+    const uint64_t nTiles = static_cast<uint64_t>(nTx) * static_cast<uint64_t>(nTy) * static_cast<uint64_t>(io.frames);
+    if (nTiles >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    TileArgs a{t, io, rowBegin, rowEnd, static_cast<int>(sb), static_cast<int>(db), nTx, nTy,
+               static_cast<unsigned>(nTiles)};
     const size_t lds = static_cast<size_t>(t.TH) * (static_cast<size_t>(t.pitchDw) * 4 + 16 + static_cast<size_t>(t.nYp) * 8) +
                        4u * static_cast<size_t>(t.CT) + static_cast<size_t>(t.srcRows) * t.spitch;
-    dim3 grid(static_cast<unsigned>((t.dstW + t.CT - 1) / t.CT), static_cast<unsigned>((rows + t.TH - 1) / t.TH),
-              static_cast<unsigned>(io.frames));
+#if IQO_TILE_XCD
+    dim3 grid(static_cast<unsigned>(nTiles));
+#else
+    dim3 grid(static_cast<unsigned>(nTx), static_cast<unsigned>(nTy), static_cast<unsigned>(io.frames));
+#endif
 #define IQO_TILE(NP_)                                                                                \
     case NP_:                                                                                        \
         kern = t.lanczos ? reinterpret_cast<const void *>(tile_kernel<NP_, true>)                    \
