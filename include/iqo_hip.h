@@ -84,8 +84,9 @@ int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
 /* Options (tests / tuning): "force_general" (0/1: every shape through IQO_KERNEL_GENERAL),
  * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
  * IQO_KERNEL_GENERAL instead of IQO_KERNEL_TILE), "tile_rows" (output rows per tile, 0 = auto),
- * "prefetch", "lin_prefetch", "stream_variant", "lanes", "chunk_frames", "debug_flags" (A/B
- * experiments; see libiqo_amd/csrc/abi.hip).  IQO_HIP_EINVAL for an unknown key or value. */
+ * "prefetch", "lin_prefetch", "stream_variant", "lanes", "chunk_frames", "xcd_order" (A/B of
+ * kernel variants and schedules, see libiqo_amd/csrc/abi.hip).  Every option changes speed only,
+ * never the output bytes.  IQO_HIP_EINVAL for an unknown key or value. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);
 
 /* Drop-in resize with HOST pointers (byte strides), synchronous: H2D, kernels, D2H. */
@@ -106,7 +107,8 @@ int iqo_hip_band_src_rows(const iqo_hip_plan *plan, size_t dstRow0, size_t dstRo
  * [dstRow0, dstRow0 + dstRows) of each frame.  dSrcWindow points at global source row srcRow0
  * (as returned by iqo_hip_band_src_rows, or any window containing it); dDstBand points at the
  * band's first row.  Rows are computed with their GLOBAL indices, so a banded result is
- * byte-identical to the unsharded one. */
+ * byte-identical to the unsharded one.  IQO_HIP_EINVAL if the window starts below the band's
+ * first source row; the kernels read no row past the end of the band's window. */
 int iqo_hip_resize_band(iqo_hip_plan *plan, size_t nFrames, size_t dstRow0, size_t dstRows,
                         size_t srcRow0, size_t srcSt, size_t srcFrameSt, const uint8_t *dSrcWindow,
                         size_t dstSt, size_t dstFrameSt, uint8_t *dDstBand, void *stream);
@@ -133,6 +135,31 @@ int iqo_hip_resize_yuv420_device(iqo_hip_yuv_plan *plan, size_t nFrames, size_t 
 int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *plan, size_t srcStY, const uint8_t *srcY, size_t srcStUV,
                           const uint8_t *srcU, const uint8_t *srcV, size_t dstStY, uint8_t *dstY, size_t dstStUV,
                           uint8_t *dstU, uint8_t *dstV);
+
+/* ---- Multi-GPU data movement for row-band / image sharding.  The reference
+ * splits a frame's output rows over OpenMP threads (src/IQOLanczosResizerImpl_AVX512.cpp:269-308);
+ * across GPUs the same split needs each band's source window (halo rows) on its device and the
+ * bands gathered back -- byte copies, no reduction, no RCCL collective.
+ *
+ * Copies nFrames blocks of bytesPerFrame bytes: block f from src + f*srcFrameSt to
+ * dst + f*dstFrameSt.  A device < 0 means host memory.  Device to device on different GPUs:
+ * hipMemcpyPeerAsync over xGMI when peer access is available, else staged through pinned host
+ * memory (synchronous).  Asynchronous on `stream` (of the destination device, or of the source
+ * device for device -> host) otherwise.  *path (may be NULL) reports the route: 0 same device,
+ * 1 peer DMA, 2 host staging, 3 host <-> device. */
+int iqo_hip_copy_frames(void *dst, int dstDevice, size_t dstFrameSt, const void *src, int srcDevice,
+                        size_t srcFrameSt, size_t bytesPerFrame, size_t nFrames, void *stream, int *path);
+
+/* Cross-process access to another process's device buffer (one process per GPU): an exported
+ * handle (64-byte hipIpcMemHandle_t + the pointer's offset in its allocation) is sent through any
+ * control channel; the receiver opens it and gets a device pointer for iqo_hip_copy_frames. */
+typedef struct {
+    unsigned char bytes[64];
+    uint64_t offset;
+} iqo_hip_ipc_handle;
+int iqo_hip_ipc_export(const void *devPtr, iqo_hip_ipc_handle *handle);
+int iqo_hip_ipc_open(const iqo_hip_ipc_handle *handle, int device, void **devPtr);
+int iqo_hip_ipc_close(void *devPtr, const iqo_hip_ipc_handle *handle);
 
 const char *iqo_hip_strerror(int status);
 const char *iqo_hip_version(void);

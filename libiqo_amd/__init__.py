@@ -12,8 +12,9 @@ call raises `IqoError`.
 import ctypes
 import os
 
-__all__ = ["IqoError", "LanczosResizer", "AreaResizer", "LinearResizer", "available", "lib",
-           "host_tables", "host_kernel_for", "host_band_src_rows", "KERNELS", "LIB_PATH"]
+__all__ = ["IqoError", "LanczosResizer", "AreaResizer", "LinearResizer", "Yuv420Resizer", "available", "lib",
+           "host_tables", "host_kernel_for", "host_band_src_rows", "copy_frames", "ipc_export", "ipc_open",
+           "ipc_close", "KERNELS", "COPY_PATHS", "LIB_PATH"]
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # LIBIQO_AMD_LIB selects an alternative build of the same library (A/B experiments only)
@@ -36,6 +37,13 @@ class PlanDesc(ctypes.Structure):
                 ("phasesX", ctypes.c_int), ("phasesY", ctypes.c_int), ("kernel", ctypes.c_int),
                 ("bandsPerFrame", ctypes.c_int)]
 
+
+class IpcHandle(ctypes.Structure):
+    """iqo_hip_ipc_handle: hipIpcMemHandle_t bytes + the pointer's offset in its allocation."""
+    _fields_ = [("bytes", ctypes.c_ubyte * 64), ("offset", ctypes.c_uint64)]
+
+
+COPY_PATHS = {0: "same device", 1: "peer DMA (xGMI)", 2: "host staging", 3: "host<->device"}
 
 _lib = None
 
@@ -78,6 +86,11 @@ def lib():
     L.iqo_hip_resize_yuv420_device.argtypes = [_vp, _c_sz, _c_sz, _c_sz, _c_sz, _vp, _vp, _vp, _c_sz, _c_sz, _c_sz,
                                                _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_int)]
     L.iqo_hip_resize_yuv420.argtypes = [_vp, _c_sz, _vp, _c_sz, _vp, _vp, _c_sz, _vp, _c_sz, _vp, _vp]
+    L.iqo_hip_copy_frames.argtypes = [_vp, ctypes.c_int, _c_sz, _vp, ctypes.c_int, _c_sz, _c_sz, _c_sz, _vp,
+                                      ctypes.POINTER(ctypes.c_int)]
+    L.iqo_hip_ipc_export.argtypes = [_vp, ctypes.POINTER(IpcHandle)]
+    L.iqo_hip_ipc_open.argtypes = [ctypes.POINTER(IpcHandle), ctypes.c_int, ctypes.POINTER(_vp)]
+    L.iqo_hip_ipc_close.argtypes = [_vp, ctypes.POINTER(IpcHandle)]
     _lib = L
     return L
 
@@ -90,6 +103,36 @@ def _check(rc, what):
 def available():
     """Number of usable gfx950 devices."""
     return int(lib().iqo_hip_available())
+
+
+def copy_frames(dst, dst_device, dst_frame_st, src, src_device, src_frame_st, bytes_per_frame, n_frames,
+                stream=None):
+    """iqo_hip_copy_frames: n_frames blocks between devices (device < 0 = host).  Returns the
+    route taken (COPY_PATHS)."""
+    path = ctypes.c_int(-1)
+    _check(lib().iqo_hip_copy_frames(_ptr(dst), dst_device, dst_frame_st, _ptr(src), src_device, src_frame_st,
+                                     bytes_per_frame, n_frames, _stream_ptr(stream), ctypes.byref(path)),
+           "copy_frames")
+    return path.value
+
+
+def ipc_export(ptr):
+    """Exportable handle (bytes) of a device buffer for another process (one process per GPU)."""
+    h = IpcHandle()
+    _check(lib().iqo_hip_ipc_export(_ptr(ptr), ctypes.byref(h)), "ipc_export")
+    return bytes(ctypes.string_at(ctypes.addressof(h), ctypes.sizeof(h)))
+
+
+def ipc_open(handle_bytes, device):
+    """Open another process's exported buffer on `device`; returns (address, handle)."""
+    h = IpcHandle.from_buffer_copy(handle_bytes)
+    p = _vp()
+    _check(lib().iqo_hip_ipc_open(ctypes.byref(h), device, ctypes.byref(p)), "ipc_open")
+    return p.value, h
+
+
+def ipc_close(addr, h):
+    _check(lib().iqo_hip_ipc_close(addr, ctypes.byref(h)), "ipc_close")
 
 
 def host_tables(method, degree, srcW, srcH, dstW, dstH, pxScale, axis):
@@ -198,6 +241,10 @@ class _Resizer:
         if out is None:
             out = torch.empty((s.shape[0], self.dstH, self.dstW), dtype=torch.uint8, device=s.device)
         o = out.unsqueeze(0) if out.dim() == 2 else out
+        if (o.dtype != torch.uint8 or o.device != s.device or tuple(o.shape) != (s.shape[0], self.dstH, self.dstW)
+                or o.stride(2) != 1 or o.stride(1) < self.dstW or (o.shape[0] > 1 and o.stride(0) < self.dstH * o.stride(1))):
+            raise IqoError("out must be a uint8 tensor [%d, %d, %d] on %s with unit column stride and "
+                           "non-overlapping rows and frames" % (s.shape[0], self.dstH, self.dstW, s.device))
         if stream is None:
             stream = torch.cuda.current_stream(s.device)
         self.resize_device(s.shape[0], s.stride(1), s.stride(0), s, o.stride(1), o.stride(0), o, stream)
@@ -286,9 +333,15 @@ class Yuv420Resizer:
         import torch
         sw, sh, dw, dh = self.srcW, self.srcH, self.dstW, self.dstH
         cs, cd = (sw // 2) * (sh // 2), (dw // 2) * (dh // 2)
+        if (src.dtype != torch.uint8 or not src.is_cuda or src.dim() != 2 or src.shape[1] != sw * sh + 2 * cs
+                or not src.is_contiguous()):
+            raise IqoError("src must be a contiguous uint8 device tensor [frames, %d]" % (sw * sh + 2 * cs))
         n = src.shape[0]
         if out is None:
             out = torch.empty((n, dw * dh + 2 * cd), dtype=torch.uint8, device=src.device)
+        if (out.dtype != torch.uint8 or out.device != src.device or tuple(out.shape) != (n, dw * dh + 2 * cd)
+                or not out.is_contiguous()):
+            raise IqoError("out must be a contiguous uint8 tensor [%d, %d] on %s" % (n, dw * dh + 2 * cd, src.device))
         b, o = src.data_ptr(), out.data_ptr()
         fused = self.resize_device(n, sw, sw // 2, src.stride(0), b, b + sw * sh, b + sw * sh + cs,
                                    dw, dw // 2, out.stride(0), o, o + dw * dh, o + dw * dh + cd, stream)

@@ -36,7 +36,8 @@ struct iqo_hip_plan {
     int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
     int linPrefetch = 0;    // Linear 2x streamer: source rows in flight per wave (0 = default 2)
     int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
-                            // streamer, 2: per-wave symmetric streamer, 3: half-width block-shared
+                            // streamer, 2: per-wave symmetric streamer (all bit-identical)
+    int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
@@ -95,6 +96,29 @@ struct HostStage {
 std::mutex g_stageMu;
 std::vector<HostStage *> g_stagePool;
 
+void destroy_stage(HostStage *st)
+{
+    for (int b = 0; b < kHostBands; ++b) {
+        if (st->evIn[b])
+            (void)hipEventDestroy(st->evIn[b]);
+        if (st->evK[b])
+            (void)hipEventDestroy(st->evK[b]);
+        if (st->evOut[b])
+            (void)hipEventDestroy(st->evOut[b]);
+    }
+    if (st->sIn)
+        (void)hipStreamDestroy(st->sIn);
+    if (st->sK)
+        (void)hipStreamDestroy(st->sK);
+    if (st->sOut)
+        (void)hipStreamDestroy(st->sOut);
+    (void)hipFree(st->dSrc);
+    (void)hipFree(st->dDst);
+    (void)hipHostFree(st->hSrc);
+    (void)hipHostFree(st->hDst);
+    delete st;
+}
+
 HostStage *acquire_stage(int device)
 {
     {
@@ -118,9 +142,8 @@ HostStage *acquire_stage(int device)
              hipEventCreateWithFlags(&st->evK[b], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&st->evOut[b], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
-        // keep what was created: the set is still returned to the pool and retried next time
-        std::lock_guard<std::mutex> g(g_stageMu);
-        g_stagePool.push_back(st);
+        // a partly built set is destroyed, never pooled: the next call builds a fresh one
+        destroy_stage(st);
         return nullptr;
     }
     return st;
@@ -418,6 +441,7 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     for (int i = 0; i < f.NX / 2 && i < 8; ++i)
         l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
     l.np = h->lanes;
+    l.xcd = h->xcdOrder;
     return l;
 }
 
@@ -518,8 +542,8 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     return kernel;
 }
 
-iqo_amd::Io make_io(size_t frames, const uint8_t *src, size_t srcSt, size_t srcFrameSt, size_t srcRow0, uint8_t *dst,
-                    size_t dstSt, size_t dstFrameSt, int dstRow0)
+iqo_amd::Io make_io(size_t frames, const uint8_t *src, size_t srcSt, size_t srcFrameSt, size_t srcRow0, int srcRowEnd,
+                    uint8_t *dst, size_t dstSt, size_t dstFrameSt, int dstRow0)
 {
     iqo_amd::Io io;
     io.frames = static_cast<int>(frames);
@@ -527,6 +551,7 @@ iqo_amd::Io make_io(size_t frames, const uint8_t *src, size_t srcSt, size_t srcF
     io.srcSt = static_cast<int64_t>(srcSt);
     io.srcFrameSt = static_cast<int64_t>(srcFrameSt);
     io.srcRow0 = static_cast<int>(srcRow0);
+    io.srcRowEnd = srcRowEnd;
     io.dst = dst;
     io.dstSt = static_cast<int64_t>(dstSt);
     io.dstFrameSt = static_cast<int64_t>(dstFrameSt);
@@ -540,10 +565,17 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
     const Plan &p = h->p;
     if (!src || !dst || srcSt < static_cast<size_t>(p.srcW) || dstSt < static_cast<size_t>(p.dstW))
         return IQO_HIP_EINVAL;
-    if (r0 + rows > static_cast<size_t>(p.dstH) || srcRow0 >= static_cast<size_t>(p.srcH))
+    const size_t dstH = static_cast<size_t>(p.dstH);
+    if (r0 > dstH || rows > dstH - r0 || srcRow0 >= static_cast<size_t>(p.srcH))
         return IQO_HIP_EINVAL;
     if (rows == 0 || nFrames == 0)
         return IQO_HIP_OK;
+    // the window must start at or above the first source row the band reads (iqo_hip_band_src_rows);
+    // the kernels read at most up to the window's end s1, never past it
+    int s0, s1;
+    iqo_amd::band_src_rows(p, static_cast<int>(r0), static_cast<int>(r0 + rows), &s0, &s1);
+    if (srcRow0 > static_cast<size_t>(s0))
+        return IQO_HIP_EINVAL;
     DeviceGuard guard(h->device);
     if (!guard.ok())
         return IQO_HIP_ENODEV;
@@ -562,7 +594,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
     }
     for (size_t f0 = 0; f0 < nFrames; f0 += chunk) {
         const iqo_amd::Io io = make_io(std::min(chunk, nFrames - f0), src + f0 * srcFrameSt, srcSt, srcFrameSt, srcRow0,
-                                       dst + f0 * dstFrameSt, dstSt, dstFrameSt, rb);
+                                       s1, dst + f0 * dstFrameSt, dstSt, dstFrameSt, rb);
         hipError_t e = hipSuccess;
         if (kernel == IQO_KERNEL_LANCZOS_STREAM)
             e = iqo_amd::launch_lanczos_stream(lanczos_dev(h), io, rb, re, h->bands, s);
@@ -648,8 +680,14 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->forceGeneral = value != 0;
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "debug_flags")) {  // timing experiments only: results are wrong
+#ifdef IQO_VARIANT_DEBUG
+    if (!std::strcmp(key, "debug_flags")) {  // variant builds only: timing experiments, wrong results
         h->debugFlags = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+#endif
+    if (!std::strcmp(key, "xcd_order")) {  // block-shared Lanczos streamer workgroup order (A/B)
+        h->xcdOrder = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "prefetch")) {  // Lanczos streamer prefetch depth (rows)
@@ -665,7 +703,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric block-shared (default), 1 ring,
-        if (value < 0 || value > 3)              // 2 symmetric per-wave, 3 half-width block-shared
+        if (value < 0 || value > 2)              // 2 symmetric per-wave
             return IQO_HIP_EINVAL;
         h->streamVariant = static_cast<int>(value);
         return IQO_HIP_OK;
@@ -924,9 +962,9 @@ int iqo_hip_resize_yuv420_device(iqo_hip_yuv_plan *yp, size_t nFrames, size_t sr
         hipError_t e = hipSuccess;
         for (size_t f0 = 0; f0 < nFrames && e == hipSuccess; f0 += chunk) {
             const size_t nf = std::min(chunk, nFrames - f0), so = f0 * srcFrameSt, dof = f0 * dstFrameSt;
-            const iqo_amd::Io iy = make_io(nf, srcY + so, srcStY, srcFrameSt, 0, dstY + dof, dstStY, dstFrameSt, 0);
-            const iqo_amd::Io iu = make_io(nf, srcU + so, srcStUV, srcFrameSt, 0, dstU + dof, dstStUV, dstFrameSt, 0);
-            const iqo_amd::Io iv = make_io(nf, srcV + so, srcStUV, srcFrameSt, 0, dstV + dof, dstStUV, dstFrameSt, 0);
+            const iqo_amd::Io iy = make_io(nf, srcY + so, srcStY, srcFrameSt, 0, py.srcH, dstY + dof, dstStY, dstFrameSt, 0);
+            const iqo_amd::Io iu = make_io(nf, srcU + so, srcStUV, srcFrameSt, 0, pc.srcH, dstU + dof, dstStUV, dstFrameSt, 0);
+            const iqo_amd::Io iv = make_io(nf, srcV + so, srcStUV, srcFrameSt, 0, pc.srcH, dstV + dof, dstStUV, dstFrameSt, 0);
             if (ky == IQO_KERNEL_LANCZOS_STREAM)
                 e = iqo_amd::launch_yuv420_lanczos(lanczos_dev(hy), iy, lanczos_dev(hc), iu, iv, s);
             else if (ky == IQO_KERNEL_AREA_INT)
@@ -967,6 +1005,158 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
     if (!rc)
         rc = iqo_hip_resize(yp->c, srcStUV, srcV, dstStUV, dstV);
     return rc;
+}
+
+// ---- multi-GPU data movement (row-band windows out, bands back; no collective)
+
+namespace {
+
+// Peer access dst -> src enabled once per process and pair (hipDeviceEnablePeerAccess is
+// per-context state; a second call reports hipErrorPeerAccessAlreadyEnabled).
+bool enable_peer(int dst, int src)
+{
+    static std::mutex mu;
+    static std::vector<std::pair<int, int>> done;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto &d : done)
+        if (d.first == dst && d.second == src)
+            return true;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, dst, src) != hipSuccess || !can)
+        return false;
+    DeviceGuard guard(dst);
+    const hipError_t e = hipDeviceEnablePeerAccess(src, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+        (void)hipGetLastError();
+        return false;
+    }
+    (void)hipGetLastError();
+    done.emplace_back(dst, src);
+    return true;
+}
+
+// nFrames blocks of `bytes` at frame strides, one 2-D copy (the frame stride is the pitch).
+hipError_t copy_blocks(void *dst, size_t dfs, const void *src, size_t sfs, size_t bytes, size_t n, hipMemcpyKind k,
+                       hipStream_t s)
+{
+    if (n == 1 || (dfs == bytes && sfs == bytes))
+        return hipMemcpyAsync(dst, src, bytes * n, k, s);
+    return hipMemcpy2DAsync(dst, dfs, src, sfs, bytes, n, k, s);
+}
+
+} // namespace
+
+int iqo_hip_copy_frames(void *dst, int dstDevice, size_t dstFrameSt, const void *src, int srcDevice, size_t srcFrameSt,
+                        size_t bytesPerFrame, size_t nFrames, void *stream, int *path)
+{
+    if (path)
+        *path = -1;
+    if (!dst || !src || (dstDevice < 0 && srcDevice < 0))
+        return IQO_HIP_EINVAL;
+    if (bytesPerFrame == 0 || nFrames == 0)
+        return IQO_HIP_OK;
+    if (nFrames > 1 && (dstFrameSt < bytesPerFrame || srcFrameSt < bytesPerFrame))
+        return IQO_HIP_EINVAL;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || dstDevice >= count || srcDevice >= count)
+        return IQO_HIP_ENODEV;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const auto u8 = [](const void *p) { return static_cast<const uint8_t *>(p); };
+    if (dstDevice < 0 || srcDevice < 0) {  // host <-> device
+        DeviceGuard guard(dstDevice >= 0 ? dstDevice : srcDevice);
+        if (!guard.ok())
+            return IQO_HIP_ENODEV;
+        const hipMemcpyKind k = srcDevice < 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+        if (copy_blocks(dst, dstFrameSt, src, srcFrameSt, bytesPerFrame, nFrames, k, s) != hipSuccess)
+            return IQO_HIP_EHIP;
+        if (path)
+            *path = 3;
+        return IQO_HIP_OK;
+    }
+    DeviceGuard guard(dstDevice);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+    if (dstDevice == srcDevice) {
+        if (copy_blocks(dst, dstFrameSt, src, srcFrameSt, bytesPerFrame, nFrames, hipMemcpyDeviceToDevice, s) != hipSuccess)
+            return IQO_HIP_EHIP;
+        if (path)
+            *path = 0;
+        return IQO_HIP_OK;
+    }
+    if (enable_peer(dstDevice, srcDevice)) {
+        // peer DMA over xGMI, one copy per frame block (contiguous blocks: one copy in all)
+        const bool contig = nFrames == 1 || (dstFrameSt == bytesPerFrame && srcFrameSt == bytesPerFrame);
+        const size_t n = contig ? 1 : nFrames, b = contig ? bytesPerFrame * nFrames : bytesPerFrame;
+        for (size_t f = 0; f < n; ++f)
+            if (hipMemcpyPeerAsync(static_cast<uint8_t *>(dst) + f * dstFrameSt, dstDevice, u8(src) + f * srcFrameSt,
+                                   srcDevice, b, s) != hipSuccess)
+                return IQO_HIP_EHIP;
+        if (path)
+            *path = 1;
+        return IQO_HIP_OK;
+    }
+    // no peer path: stage through pinned host memory, block by block (synchronous)
+    uint8_t *h = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void **>(&h), bytesPerFrame, hipHostMallocDefault) != hipSuccess)
+        return IQO_HIP_ENOMEM;
+    int rc = IQO_HIP_OK;
+    for (size_t f = 0; f < nFrames && rc == IQO_HIP_OK; ++f) {
+        {
+            DeviceGuard sg(srcDevice);
+            if (!sg.ok() || hipMemcpy(h, u8(src) + f * srcFrameSt, bytesPerFrame, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = IQO_HIP_EHIP;
+        }
+        if (rc == IQO_HIP_OK &&
+            hipMemcpy(static_cast<uint8_t *>(dst) + f * dstFrameSt, h, bytesPerFrame, hipMemcpyHostToDevice) != hipSuccess)
+            rc = IQO_HIP_EHIP;
+    }
+    (void)hipHostFree(h);
+    if (path && rc == IQO_HIP_OK)
+        *path = 2;
+    return rc;
+}
+
+int iqo_hip_ipc_export(const void *devPtr, iqo_hip_ipc_handle *handle)
+{
+    static_assert(sizeof(hipIpcMemHandle_t) <= sizeof(handle->bytes), "IPC handle size");
+    if (!devPtr || !handle)
+        return IQO_HIP_EINVAL;
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange(&base, &size, const_cast<void *>(devPtr)) != hipSuccess || !base)
+        return IQO_HIP_EHIP;
+    hipIpcMemHandle_t h;
+    if (hipIpcGetMemHandle(&h, base) != hipSuccess)
+        return IQO_HIP_EHIP;
+    std::memset(handle, 0, sizeof(*handle));
+    std::memcpy(handle->bytes, &h, sizeof(h));
+    handle->offset = static_cast<uint64_t>(static_cast<const uint8_t *>(devPtr) - static_cast<const uint8_t *>(base));
+    return IQO_HIP_OK;
+}
+
+int iqo_hip_ipc_open(const iqo_hip_ipc_handle *handle, int device, void **devPtr)
+{
+    if (!handle || !devPtr)
+        return IQO_HIP_EINVAL;
+    *devPtr = nullptr;
+    DeviceGuard guard(device);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handle->bytes, sizeof(h));
+    void *base = nullptr;
+    if (hipIpcOpenMemHandle(&base, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess || !base)
+        return IQO_HIP_EHIP;
+    *devPtr = static_cast<uint8_t *>(base) + handle->offset;
+    return IQO_HIP_OK;
+}
+
+int iqo_hip_ipc_close(void *devPtr, const iqo_hip_ipc_handle *handle)
+{
+    if (!devPtr || !handle)
+        return IQO_HIP_EINVAL;
+    return hipIpcCloseMemHandle(static_cast<uint8_t *>(devPtr) - handle->offset) == hipSuccess ? IQO_HIP_OK
+                                                                                                : IQO_HIP_EHIP;
 }
 
 const char *iqo_hip_strerror(int status)

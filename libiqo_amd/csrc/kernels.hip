@@ -27,6 +27,25 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
 
+// Timing-experiment flags (drop stores / loads / border work: WRONG output).  They exist only
+// in the variant builds of scripts/build_variant.sh (-DIQO_VARIANT_DEBUG); the shipping library
+// compiles every flag test away, so no public option can change its results.
+#ifdef IQO_VARIANT_DEBUG
+#define IQO_DBG(a) ((a).dbg)
+#else
+#define IQO_DBG(a) 0
+#endif
+
+// Workgroups are dealt round-robin over the 8 XCDs (flat id L runs on XCD L mod 8; placement is
+// a speed property only, never relied on for correctness).  xcd_spread maps the flat id to a
+// logical id so that XCD x receives the contiguous logical range [s_x, s_x + c_x), a bijection
+// of [0, n) for any n.
+__device__ __forceinline__ unsigned xcd_spread(unsigned L, unsigned n)
+{
+    const unsigned xcd = L & 7u, idx = L >> 3, q = n >> 3, r = n & 7u;
+    return xcd < r ? xcd * (q + 1u) + idx : r * (q + 1u) + (xcd - r) * q + idx;
+}
+
 // 16-byte streaming load (source pixels are read once per band): nontemporal hint.
 __device__ __forceinline__ uint4 load16_nt(const uint8_t *p)
 {
@@ -286,9 +305,7 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     // rows / columns they share are fetched from HBM once and hit that XCD's L2 afterwards.
     int tileX, tileY, frame;
     {
-        const unsigned L = blockIdx.x, N = a.nTiles;
-        const unsigned xcd = L & 7u, idx = L >> 3, q = N >> 3, r = N & 7u;
-        const unsigned lg = xcd < r ? xcd * (q + 1u) + idx : r * (q + 1u) + (xcd - r) * q + idx;
+        const unsigned lg = xcd_spread(blockIdx.x, a.nTiles);
 #if IQO_TILE_XCD == 2  // A/B: column tiles fastest
         const unsigned rest = lg / static_cast<unsigned>(a.nTx);
         tileX = static_cast<int>(lg - rest * static_cast<unsigned>(a.nTx));
@@ -535,11 +552,12 @@ struct LanczosArgs {
     int rowBegin, rowEnd, rowsPerBand;
     int srcBytes, dstBytes;  // extent of one frame's source window / destination band (buffer range)
     int bands, wavesPerRow;  // wave grid per frame: band-major, column-minor
-    int dbg;                 // timing experiments only (plan option "debug_flags"): 1 = no stores,
+    int dbg;                 // variant builds only (IQO_DBG): 1 = no stores,
                              // 2 = no source loads, 4 = no edge columns, 8 = no border rows
                              // (wrong output), 32 = all bands walk top-down.  0 in production.
     int np;                  // producing lanes per wave (symmetric streamer)
     int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
+    int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -614,7 +632,7 @@ __device__ __forceinline__ void lanczos_stream_kernel_body(const LanczosArgs &a,
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0;
-    const int dbg = a.dbg;
+    const int dbg = IQO_DBG(a);
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
     const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;  // dropped for non-producers
 
@@ -780,7 +798,10 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 
 // 16-byte-per-lane LDS-DMA of one source row into LDS bytes [lds, lds + 1024) of this wave.
 // M0 is saved and restored inside the statement (it is compiler-reserved).
-__device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff, bool nt = true)
+#ifndef IQO_DMA_NT
+#define IQO_DMA_NT 1  // nontemporal LDS-DMA source reads (each source row is read once)
+#endif
+__device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff, bool nt = IQO_DMA_NT)
 {
     uint32_t keep;
     if (nt)
@@ -803,11 +824,6 @@ __device__ __forceinline__ void wait_vmcnt()
     static_assert(N >= 0 && N < 64, "vmcnt field");
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-
-// cache policy of the symmetric streamer's output stores (experiments: 2 = nontemporal)
-#ifndef IQO_SYM_STORE_AUX
-#define IQO_SYM_STORE_AUX 0
-#endif
 
 template <int NY, int NX, int OFFX, int K, bool C0ONE>
 __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
@@ -840,7 +856,7 @@ __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, co
     const int outX = x0 + (lane - 1) * 8;
     const bool produce = lane >= 1 && lane <= np && outX < L.dstW;
     const int voff = (lane <= np + 1 && cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;
-    const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
+    const bool edgeL = x0 == 0 && !(IQO_DBG(a) & 4), edgeR = x0 + opw >= L.dstW && !(IQO_DBG(a) & 4);
     const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
@@ -850,7 +866,7 @@ __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, co
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0;
-    const int dbg = a.dbg;
+    const int dbg = IQO_DBG(a);
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
     const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
     // Odd bands walk bottom-up: a band boundary's halo rows are then read by both bands at the
@@ -956,11 +972,6 @@ __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, co
         uint4 n0, n1;
         read_iter(i, n0, n1);
         dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
-#ifdef IQO_EXP_MEMONLY  // timing experiment: memory stream only (wrong output)
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{n0.x ^ n1.y, n0.z ^ n1.w}, dstR, stoff, (yy - a.io.dstRow0) * dstSt,
-                                              IQO_SYM_STORE_AUX);
-        return;
-#endif
         unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
         unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
 
@@ -1015,7 +1026,7 @@ __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, co
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, IQO_SYM_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every 64 rows and at the band end one pass divides them, one row per lane
@@ -1107,7 +1118,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const bool produce = lane >= 1 && lane <= np && outX < L.dstW;
     const int voff = (lane <= np + 1 && cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;  // prologue loads
     const int ldsCol = lane <= np + 1 ? 16 + cb : 0;  // this lane's 16 bytes in an LDS ring row
-    const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
+    const bool edgeL = x0 == 0 && !(IQO_DBG(a) & 4), edgeR = x0 + opw >= L.dstW && !(IQO_DBG(a) & 4);
     const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
@@ -1117,7 +1128,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0;
-    const int dbg = a.dbg;
+    const int dbg = IQO_DBG(a);
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
     const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
     // Odd bands walk bottom-up: a band boundary's halo rows are then read by both bands at the
@@ -1257,26 +1268,13 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         // this wave's DMA(i) retired: after it come the store of iteration i-K+1 and the 2*CPW
         // DMAs + 1 store of each of iterations i-K+2 .. i-1; then the workgroup barrier makes
         // every wave's chunks of iteration i visible and retires all reads of slot (i-1) mod K
-#ifdef IQO_EXP_SETPRIO
-        __builtin_amdgcn_s_setprio(IQO_EXP_SETPRIO);
-#endif
         wait_vmcnt<WAIT>();
         asm volatile("" ::: "memory");
-#ifndef IQO_EXP_NOBARRIER  // timing experiment only (races: wrong output)
         __builtin_amdgcn_s_barrier();
-#endif
         asm volatile("" ::: "memory");
         uint4 n0, n1;
         read_iter(i, n0, n1);
         dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
-#endif
-#ifdef IQO_EXP_SETPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
-#ifdef IQO_EXP_MEMONLY  // timing experiment: memory stream only (wrong output)
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2{n0.x ^ n1.y, n0.z ^ n1.w}, dstR, stoff, (yy - a.io.dstRow0) * dstSt,
-                                              IQO_SYM_STORE_AUX);
-        return;
 #endif
         unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
         unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
@@ -1373,7 +1371,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, IQO_SYM_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every 64 rows and at the band end one pass divides them, one row per lane
@@ -1396,249 +1394,19 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WAVES_PER_EU))) void lanczos_symb_kernel(LanczosArgs a)
 {
-    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, blockIdx.x, blockIdx.y);
-}
-
-
-#ifndef IQO_SYMH_WAVES_PER_EU
-#define IQO_SYMH_WAVES_PER_EU 6
-#endif
-// ================================================================ half-width symmetric streamer
-//
-// The block-shared streamer with 8 source columns (4 outputs) per lane instead of 16 (8): the
-// register window is half as large (10 rows x 4 u16 pairs), so the kernel fits 6 waves per SIMD
-// instead of 4 and hides more of the HBM latency behind the other waves' arithmetic, at the cost
-// of more DPP traffic per output (neighbour pairs and the unpack's right byte).  Same ring, same
-// border semantics, same walk (see lanczos_symb_kernel_body); a workgroup is the wpr <= 8 waves
-// of one row band.
-
-template <int NY, int NX, int OFFX, int K, bool C0ONE>
-__device__ __forceinline__ void lanczos_symh_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
-{
-    constexpr int H = NY / 2;
-    static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
-    static_assert(K >= 3, "ring depth (look-ahead)");
-    constexpr int WAIT = 1 + (K - 2) * 3;    // vm ops issued after this wave's DMA(i) (2 DMAs + 1 store per iteration)
-    constexpr int WAITLA = 1 + (K - 3) * 3;  // ... after DMA(i+1)
-    constexpr int JLO = (OFFX + 1) / 2;      // output k, tap pair p reads Q_{k + p + JLO}
-    static_assert(JLO >= -3 && 3 + NX / 2 - 1 + JLO <= 8, "taps must stay within the neighbouring lanes");
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int rowPitch = a.rowPitch, slotBytes = 2 * rowPitch;
-    uint8_t *const ring = lds;
-    int4 (*const edgeSum)[64] = reinterpret_cast<int4 (*)[64]>(lds + K * slotBytes);
-    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + 2 * 64 * 16);
-
-    const LanczosDev &L = a.l;
-    const int lane = static_cast<int>(threadIdx.x) & 63;
-    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const int band = static_cast<int>(bx), wcol = wib;
-    const int y0 = a.rowBegin + band * a.rowsPerBand;
-    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
-    if (y0 >= y1)
-        return;  // whole workgroup
-
-    const int np = a.np, opw = 4 * np;
-    const int x0 = max(0, min(wcol * opw, L.dstW - opw));
-    const int cb = 2 * x0 - 8 + 8 * lane;       // first source column of this lane (8 columns)
-    const int outX = x0 + (lane - 1) * 4;        // first output column of this lane (4 outputs)
-    const bool produce = lane >= 1 && lane <= np && outX < L.dstW;
-    const int voff = (lane <= np + 1 && cb >= 0 && cb < L.srcW) ? cb : 0x7ff00000;  // prologue loads
-    const int ldsCol = lane <= np + 1 ? 16 + cb : 0;
-    const bool edgeL = x0 == 0 && !(a.dbg & 4), edgeR = x0 + opw >= L.dstW && !(a.dbg & 4);
-    const bool laneL = outX == 0, laneR = outX == L.dstW - 4;
-
-    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
-    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
-    const __amdgpu_buffer_rsrc_t srcR =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
-    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
-    const int srcRow0 = a.io.srcRow0;
-    const int dbg = a.dbg;
-    const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
-    const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
-    const int dir = ((band & 1) && !(dbg & 32)) ? -1 : 1;
-    const int rFirst = 2 * y0 + L.offY;
-    const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;
-    const int nRows = y1 - y0;
-    const uint32_t bias = opaque(1u << 19);
-    uint32_t cvx[NX / 2];  // X coefficient pairs in VGPRs (VOP2 DPP needs a VGPR src1)
-#pragma unroll
-    for (int p = 0; p < NX / 2; ++p)
-        cvx[p] = opaque(L.cxo[p]);
-
-    const uint32_t ldsBase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
-        (__attribute__((address_space(3))) uint8_t *)lds));
-    const uint8_t *ringLane = ring + ldsCol;
-    auto row_soff = [&](int r) { return (r >= rFirst && r <= rLast) ? (r - srcRow0) * srcSt : 0x7ff00000; };
-    auto rowAt = [&](int i, int t) { return dir > 0 ? rFirst + 2 * i + t : rLast - 2 * i - t; };
-    auto dma_iter = [&](int i) {
-        const uint32_t sl = ldsBase + static_cast<uint32_t>((i % K) * slotBytes);
-        const int r = rowAt(i, NY - 2);
-        const int c = wcol;
-        const bool real = c < a.chunks;  // uniform; otherwise a same-count DMA into the sink
-        const int col = 1024 * c + 16 * lane;
-        const int v = (real && col < L.srcW && !(dbg & 2)) ? col : 0x7ff00000;
-        const uint32_t d0 = real ? sl + 16 + 1024 * c : ldsBase + sinkLds;
-        const uint32_t d1 = real ? d0 + rowPitch : d0;
-        dma_row(d0, v, srcR, row_soff(r));
-        dma_row(d1, v, srcR, row_soff(r + dir));
-    };
-    auto read_iter = [&](int i, uint2 &r0, uint2 &r1) {
-        const uint8_t *pp = ringLane + (i % K) * slotBytes;
-        r0 = *reinterpret_cast<const uint2 *>(pp);
-        r1 = *reinterpret_cast<const uint2 *>(pp + rowPitch);
-    };
-    // odd-aligned u16 pairs Q_1..Q_4 of one row: (b1,b2) (b3,b4) (b5,b6) (b7,b8), b8 = right
-    // neighbour's byte 0
-    auto unpack_odd4 = [&](uint2 v, uint32_t (&q)[4]) {
-        const uint32_t r = static_cast<uint32_t>(
-            __builtin_amdgcn_mov_dpp(static_cast<int>(v.x), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
-        q[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c020c01u);
-        q[1] = __builtin_amdgcn_perm(v.y, v.x, 0x0c040c03u);
-        q[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c020c01u);
-        q[3] = __builtin_amdgcn_perm(r, v.y, 0x0c040c03u);
-    };
-    auto flush_edges = [&](int yb, int n) {
-        auto fix = [&](int sv, int k) {
-            const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.xM[k]) >> L.xT[k];
-            return min(qq, 255u);
-        };
-        const int rowOff = (yb + dir * lane - a.io.dstRow0) * dstSt;
-        if (edgeL) {
-            const int4 e = edgeSum[0][lane & 63];
-            const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
-            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff : 0x7ff00000, 0, 0);
-        }
-        if (edgeR) {
-            const int4 e = edgeSum[1][lane & 63];
-            const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
-            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff + L.dstW - 4 : 0x7ff00000,
-                                                  0, 0);
-        }
-    };
-
-    uint32_t win[NY][4];
-    {
-        uint2 w0[NY - 2];
-#pragma unroll
-        for (int t = 0; t < NY - 2; ++t) {
-            u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(srcR, svoff, row_soff(rowAt(0, t)), 2 /* nt */);
-            w0[t] = make_uint2(q.x, q.y);
-        }
-#pragma unroll
-        for (int t = 0; t < NY - 2; ++t)
-            unpack_odd4(w0[t], win[t]);
+    unsigned bx = blockIdx.x, by = blockIdx.y;
+    if (a.xcd) {
+        // XCD-aware order (speed only): the band workgroups of one frame go to one XCD, so the
+        // halo rows two neighbouring bands share hit that XCD's L2, and each XCD streams from
+        // 1/8 of the batch's address range
+        const unsigned bands = gridDim.x;
+        const unsigned lg = xcd_spread(by * bands + bx, bands * gridDim.y);
+        by = lg / bands;
+        bx = lg - by * bands;
     }
-    for (int r = static_cast<int>(threadIdx.x); r < 2 * K; r += static_cast<int>(blockDim.x))
-        *reinterpret_cast<uint4 *>(ring + r * rowPitch) = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int j = 0; j < K - 1; ++j) {
-        dma_iter(j);
-        __builtin_amdgcn_raw_buffer_store_b32(0u, dstR, 0x7ff00000, 0, 0);
-    }
-    uint2 n0, n1;
-    wait_vmcnt<WAIT>();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    read_iter(0, n0, n1);
-
-    auto row = [&](auto uc, int base) {
-        constexpr int v = decltype(uc)::value;
-        const int i = base + v;
-        if (i >= nRows)
-            return;
-        const int yy = dir > 0 ? y0 + i : y1 - 1 - i;
-        wait_vmcnt<WAITLA>();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        uint2 m0, m1;
-        read_iter(i + 1, m0, m1);
-        dma_iter(i + K - 1);
-        unpack_odd4(n0, win[(2 * v + NY - 2) % NY]);
-        unpack_odd4(n1, win[(2 * v + NY - 1) % NY]);
-        n0 = m0;
-        n1 = m1;
-
-        uint32_t acc[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const uint32_t p0 = win[(2 * v) % NY][c] + win[(2 * v + NY - 1) % NY][c];
-            acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
-        }
-#pragma unroll
-        for (int p = 1; p < H; ++p)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
-                acc[c] = pk_mad(pp, L.cy[p], acc[c]);
-            }
-        if ((yy < L.mainBeginY || yy >= L.mainEndY) && !(dbg & 8)) {
-            const bool top = yy < L.mainBeginY;
-            const int bi = top ? yy : yy - L.mainEndY;
-            const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
-            const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                acc[c] = ydiv2(acc[c], m, sh);
-        }
-
-        // horizontal: own pairs Q_1..Q_4 = acc[0..3]; neighbour pairs through DPP-modified dots
-        asm volatile("s_nop 1" ::: "memory");
-        int sum[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            int pFirst = -1;
-#pragma unroll
-            for (int p = 0; p < NX / 2; ++p) {
-                const int j = k + p + JLO;
-                if (pFirst < 0 && j >= 1 && j <= 4)
-                    pFirst = p;
-            }
-            int sacc;
-            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[pFirst]), "v"(acc[k + pFirst + JLO - 1]),
-                "v"(bias));
-#pragma unroll
-            for (int p = 0; p < NX / 2; ++p) {
-                const int j = k + p + JLO;
-                if (p == pFirst)
-                    continue;
-                if (j <= 0)
-                    asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
-                        : "+v"(sacc) : "v"(acc[j + 3]), "v"(cvx[p]));
-                else if (j >= 5)
-                    asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf"
-                        : "+v"(sacc) : "v"(acc[j - 5]), "v"(cvx[p]));
-                else
-                    sacc = sdot2(acc[j - 1], L.cxo[p], sacc);
-            }
-            sum[k] = sacc;
-        }
-        const uint32_t o = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
-        __builtin_amdgcn_raw_buffer_store_b32(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
-        if (edgeL || edgeR) {
-            const int slot = i & (IQO_SYMB_EDGE_BATCH - 1);
-            if ((edgeL && laneL) || (edgeR && laneR))
-                edgeSum[laneL ? 0 : 1][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
-            if (slot == IQO_SYMB_EDGE_BATCH - 1 || i == nRows - 1) {
-                __builtin_amdgcn_wave_barrier();
-                flush_edges(yy - dir * slot, slot + 1);
-            }
-        }
-    };
-    for (int base = 0; base < nRows; base += H)
-        static_for<H>([&](auto uc) { row(uc, base); });
-
-    wait_vmcnt<0>();
+    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, bx, by);
 }
-template <int NY, int NX, int OFFX, int K, bool C0ONE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_SYMH_WAVES_PER_EU))) void
-lanczos_symh_kernel(LanczosArgs a)
-{
-    lanczos_symh_kernel_body<NY, NX, OFFX, K, C0ONE>(a, blockIdx.x, blockIdx.y);
-}
+
 
 // ================================================================ Area integer ratio
 //
@@ -2037,7 +1805,7 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
     const int rows = rowEnd - rowBegin;
-    const int64_t sb = static_cast<int64_t>(t.srcH - io.srcRow0 - 1) * io.srcSt + t.srcW;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + t.srcW;
     const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + t.dstW;
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24) ||
         io.dstSt >= (int64_t(1) << 31) || t.srcH >= (1 << 24))
@@ -2107,17 +1875,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     int opw = 62 * (16 / l.KX);
     int wpr = (l.dstW + opw - 1) / opw;
     int np = 62;
-    const bool half = l.sym == 3;
-    if (half) {
-        // half-width lanes: 4 outputs per lane (1920 -> 8 waves x 60 lanes x 4 outputs)
-        const int lanes = (l.dstW + 3) / 4;
-        wpr = (lanes + 61) / 62;
-        np = l.np > 0 ? min(l.np, 62) : (lanes + wpr - 1) / wpr;
-        if (np * 4 > l.dstW)
-            np = l.dstW / 4;
-        opw = 4 * np;
-        wpr = (l.dstW + opw - 1) / opw;
-    } else if (l.sym) {
+    if (l.sym) {
         // producing lanes per wave: the fewest waves per row, then the fewest lanes that still
         // tile the output width (1920 -> 4 waves x 60 lanes x 8 outputs, no overlap)
         const int lanes = (l.dstW + 7) / 8;
@@ -2134,23 +1892,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int chunks = (l.srcW + 16 + 1023) / 1024;
     const int cpw = (chunks + wpr - 1) / wpr;
     const int rowPitch = 16 + 1024 * chunks;
-    const bool shared = l.sym && l.sym != 2 && (half ? wpr <= 8 && cpw <= 1 : wpr <= 4 && cpw <= 2);
-    if (shared && half) {
-        const bool one = (l.cy[0] & 0xffffu) == 1u;
-        const int K = pd <= 2 ? 3 : 4;
-        ldsBytes = K * 2 * rowPitch + 2 * 64 * 16 + 1024;
-        block = 64 * wpr;
-#define IQO_SYMH(NY_, NX_, OX_, ONE_)                                                 \
-    (K == 3 ? reinterpret_cast<const void *>(lanczos_symh_kernel<NY_, NX_, OX_, 3, ONE_>) \
-            : reinterpret_cast<const void *>(lanczos_symh_kernel<NY_, NX_, OX_, 4, ONE_>))
-        if (l.NY == 10 && one)
-            kern = IQO_SYMH(10, 12, -5, true);
-        else if (l.NY == 10)
-            kern = IQO_SYMH(10, 12, -5, false);
-        else
-            kern = IQO_SYMH(8, 8, -3, false);
-#undef IQO_SYMH
-    } else if (shared) {
+    const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
+    if (shared) {
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         const int K = pd <= 2 ? 3 : 4;
@@ -2169,16 +1912,6 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB
     } else if (l.sym) {
-        if (half) {  // not eligible for the half-width kernel: the per-wave symmetric streamer
-            const int lanes = (l.dstW + 7) / 8;
-            opw = 62 * 8;
-            wpr = (l.dstW + opw - 1) / opw;
-            np = l.np > 0 ? min(l.np, 62) : (lanes + wpr - 1) / wpr;
-            if (np * 8 > l.dstW)
-                np = l.dstW / 8;
-            opw = 8 * np;
-            wpr = (l.dstW + opw - 1) / opw;
-        }
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         if (l.NY == 10 && one)
             kern = pd <= 2 ? reinterpret_cast<const void *>(lanczos_sym_kernel<10, 12, -5, 3, true>)
@@ -2207,10 +1940,10 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
-    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks};
-    // buffer ranges: the source window spans rows [srcRow0, srcH) of the frame, the destination
+    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd};
+    // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
-    const int64_t sb = static_cast<int64_t>(l.srcH - io.srcRow0 - 1) * io.srcSt + l.srcW;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;
     const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + l.dstW;
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 31) ||
         io.dstSt >= (int64_t(1) << 31))
@@ -2275,9 +2008,9 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
     int wpr = (lanes + 61) / 62;
     int np = (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
-    // nontemporal stores by default (dbg 16 = plain stores, for A/B); 2 rows in flight per wave
-    // measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
-    const bool nt = !(g.dbg & 16);
+    // nontemporal stores by default (variant builds: dbg 16 = plain stores, for A/B); 2 rows in
+    // flight per wave measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
+    const bool nt = !(IQO_DBG(g) & 16);
     const int pd = g.prefetch == 0 ? 2 : g.prefetch;
     const void *kern = pd >= 8 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<8, true>)
                                      : reinterpret_cast<const void *>(linear_up2_kernel<8, false>))
@@ -2292,7 +2025,7 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
     bands = (rows + rpb - 1) / rpb;
     LinearArgs &a = P->a;
     a = LinearArgs{g, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, np};
-    const int64_t sb = static_cast<int64_t>(g.srcH - io.srcRow0 - 1) * io.srcSt + g.srcW;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + g.srcW;
     const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + g.dstW;
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31))
         return hipErrorInvalidValue;

@@ -13,6 +13,7 @@ struct Io {
     const uint8_t *src;
     int64_t srcSt, srcFrameSt;
     int srcRow0;
+    int srcRowEnd;  // one past the last global source row the call may read (end of the window)
     uint8_t *dst;
     int64_t dstSt, dstFrameSt;
     int dstRow0;
@@ -58,13 +59,14 @@ struct LanczosDev {
     uint32_t yTopM[16], yBotM[16], xM[8];
     int yTopS[16], yBotS[16], xT[8];
     int yTopNeg, yBotNeg, xNeg;  // bit i: border row / column i has a negative denominator
-    int dbg;                     // timing experiments only (see kernels.hip)
+    int dbg;                     // variant builds only (kernels.hip IQO_DBG); ignored otherwise
     int prefetch;                // prefetch depth in output rows (1..3)
     // symmetric streamer (plan.hpp FastLanczos::sym)
-    int sym;                     // 1: block-shared symmetric, 2: per-wave symmetric, 3: half-width block-shared, 0: accumulator ring
+    int sym;                     // 1: block-shared symmetric, 2: per-wave symmetric, 0: accumulator ring
     int NX, offXO;               // unpadded X taps, odd first tap column
     uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table
     int np;                      // producing lanes per wave (0 = auto)
+    int xcd;                     // block-shared streamer: XCD-aware workgroup order (speed only)
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
@@ -84,7 +86,7 @@ struct LinearDev {
     int srcW, srcH, dstW, dstH;
     uint32_t cy[2];              // per phase (c0, c1) u16 pairs
     uint32_t cx[2];
-    int dbg;                     // timing experiments: 16 = plain (not nontemporal) stores
+    int dbg;                     // variant builds only: 16 = plain (not nontemporal) stores
     int prefetch;                // source rows in flight per wave (2, 4, 8; 0 = default 2)
 };
 hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, int bands,

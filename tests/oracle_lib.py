@@ -81,6 +81,50 @@ def ref(strict=False):
     return _ref[key]
 
 
+def ref_cpu_available():
+    return os.path.exists(os.path.join(REF_DIR, "libiqo_ref_cpu.so"))
+
+
+def ref_cpu():
+    """The reference's whole CPU library (CPUID dispatch + OpenMP; oracle/ref_cpu_harness.cpp):
+    a SPEED baseline only -- its SIMD paths are f32 and not bit-exact with Generic.
+
+    libgomp reads OMP_WAIT_POLICY when it loads: passive waiting is set first, since spinning
+    OpenMP threads on a CPU-quota'd host (the GPU box: 16 CPUs of quota in a 256-CPU affinity
+    mask) or on shared vCPUs stall each other (measured: 8 active-spin threads 13x slower than
+    one thread in the build container; passive 4.7x faster)."""
+    if "cpu" not in _ref:
+        os.environ.setdefault("OMP_WAIT_POLICY", "passive")
+        lib = _load(os.path.join(REF_DIR, "libiqo_ref_cpu.so"))
+        lib.iqo_refcpu_arch.restype = ctypes.c_char_p
+        for f in ("iqo_refcpu_run_rows", "iqo_refcpu_run_frames"):
+            fn = getattr(lib, f)
+            fn.restype = ctypes.c_double
+            fn.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz, _c_sz,
+                           _u8p, _c_sz, _c_sz, _u8p, ctypes.c_int]
+        lib.iqo_refcpu_bench_yuv420.restype = ctypes.c_double
+        lib.iqo_refcpu_bench_yuv420.argtypes = [ctypes.c_int, ctypes.c_uint, _c_sz, _c_sz, _c_sz, _c_sz, ctypes.c_int,
+                                                ctypes.c_int, _u8p, _u8p, _u8p, _c_sz, _c_sz, _u8p, _u8p, _u8p,
+                                                _c_sz, _c_sz]
+        _ref["cpu"] = lib
+    return _ref["cpu"]
+
+
+def host_cpus():
+    """(affinity CPUs, cgroup CPU quota or None, usable CPUs = min of the two)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(p)
+    except (OSError, ValueError):
+        pass
+    usable = aff if quota is None else max(1, min(aff, int(quota)))
+    return aff, quota, usable
+
+
 def ref_tables_lib(strict=False):
     key = "tstrict" if strict else "trel"
     if key not in _ref:

@@ -157,6 +157,131 @@ def test_row_band_sharding_is_byte_identical(cfg):
     assert torch.equal(torch.cat(parts, dim=1), full)
 
 
+def test_band_window_must_cover_the_halo():
+    """A window that starts one row too late is rejected (it would silently read zeros)."""
+    r = libiqo_amd.LanczosResizer(3, 3840, 2160, 1920, 1080)
+    s0, sn = r.band_src_rows(500, 100)
+    src = torch.zeros((1, sn, 3840), dtype=torch.uint8, device=DEV)
+    band = torch.empty((1, 100, 1920), dtype=torch.uint8, device=DEV)
+    with pytest.raises(libiqo_amd.IqoError):
+        r.resize_band(1, 500, 100, s0 + 1, 3840, sn * 3840, src, 1920, 100 * 1920, band)
+    with pytest.raises(libiqo_amd.IqoError):  # r0 + rows past the frame (no size_t wrap)
+        r.resize_band(1, 1000, 2 ** 64 - 10, s0, 3840, sn * 3840, src, 1920, 100 * 1920, band)
+    r.resize_band(1, 500, 100, s0, 3840, sn * 3840, src, 1920, 100 * 1920, band)
+    torch.cuda.synchronize()
+
+
+def _orchestrated(cfg, devices, host_src, frames=3, seed=5):
+    from libiqo_amd import shard
+
+    m, d, sw, sh, dw, dh, px = cfg
+    g = torch.Generator(device=DEV)
+    g.manual_seed(seed)
+    src = torch.randint(0, 256, (frames, sh, sw), dtype=torch.uint8, device=DEV, generator=g)
+    full = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px).resize_tensor(src)
+    out = torch.zeros((frames, dh, dw), dtype=torch.uint8, device=DEV)
+    s = src.cpu().pin_memory() if host_src else src
+    be = shard.HipBandBackend(lambda dev: libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px, device=dev),
+                              s, -1 if host_src else 0, out, 0)
+    shards = shard.make_shards(be.resizer(0), dh, devices)
+    times = shard.run_bands_local(be, shards)
+    torch.cuda.synchronize()
+    return full, out, times, be
+
+
+@pytest.mark.parametrize("cfg", CONFIGS[:3] + [CONFIGS[5]], ids=["c2", "c3", "c4", "lz3up"])
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0, 0, 0]], ids=["1band", "2bands", "5bands"])
+def test_band_orchestrator_local_matches_unsharded(cfg, devices):
+    """libiqo_amd.shard with the HIP backend: windows out (device 0 -> shard device by
+    iqo_hip_copy_frames), iqo_hip_resize_band per shard, bands gathered back -- byte-identical to
+    the unsharded launch.  On a one-GPU box the shards share device 0."""
+    full, out, times, be = _orchestrated(cfg, devices, host_src=False)
+    assert torch.equal(out, full)
+    assert all(v >= 0 for v in times.values())
+    assert be.paths["scatter"] == {"same device"} and be.paths["gather"] == {"same device"}
+
+
+def test_band_orchestrator_host_source():
+    """Windows uploaded from pinned host memory (the H2D route of iqo_hip_copy_frames)."""
+    full, out, times, be = _orchestrated(CONFIGS[0], [0, 0, 0], host_src=True)
+    assert torch.equal(out, full)
+    assert be.paths["scatter"] == {"host<->device"}
+
+
+def _ipc_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+    from libiqo_amd import shard
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # control channel only
+    try:
+        m, d, sw, sh, dw, dh, px = CONFIGS[0]
+        torch.cuda.set_device(0)
+        g = torch.Generator(device="cuda:0")
+        g.manual_seed(11)
+        src = torch.randint(0, 256, (2, sh, sw), dtype=torch.uint8, device="cuda:0", generator=g)
+        out = torch.zeros((2, dh, dw), dtype=torch.uint8, device="cuda:0") if rank == 0 else None
+        be = shard.HipBandBackend(lambda dev: libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px, device=dev),
+                                  src, 0, out, 0)
+        shards = shard.make_shards(be.resizer(0), dh, [0] * world)
+        times, band = shard.run_bands_distributed(be, shards, rank, world, dist)
+        ok = True
+        if rank == 0:
+            full = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px).resize_tensor(src)
+            torch.cuda.synchronize()
+            ok = bool(torch.equal(out, full))
+        q.put((rank, ok, sorted(be.paths.get("gather", []))))
+    except Exception as e:  # report, do not hang the parent
+        q.put((rank, repr(e), []))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_band_orchestrator_distributed_ipc():
+    """One process per shard (2 ranks, both on cuda:0 of the one-GPU box; gloo carries only the
+    IPC handles): rank 1's band reaches rank 0's output through iqo_hip_ipc_export / _open and a
+    device copy -- no collective on the pixels."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ipc_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, ok, paths = q.get(timeout=100)
+        res[r] = (ok, paths)
+    for p in procs:
+        p.join(timeout=30)
+    assert res[0][0] is True and res[1][0] is True, res
+
+
+def test_256_frame_batch_bit_exact():
+    """BASELINE.md §4 batch size for C2: one launch over 256 frames; frames 0, 128, 255 against
+    the oracle."""
+    sw, sh, dw, dh = 3840, 2160, 1920, 1080
+    g = torch.Generator(device=DEV)
+    g.manual_seed(256)
+    src = torch.randint(0, 256, (256, sh, sw), dtype=torch.uint8, device=DEV, generator=g)
+    out = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh).resize_tensor(src)
+    torch.cuda.synchronize()
+    for f in (0, 128, 255):
+        exp = ol.run_oracle("lanczos", 3, sw, sh, dw, dh, 1, src[f].cpu().numpy())
+        assert (out[f].cpu().numpy() == exp).all(), f
+    del src, out
+    torch.cuda.empty_cache()
+
+
 STREAM_SHAPES = [
     (3, 3840, 2160, 1920, 1080),  # C2: 4 waves x 60 lanes per row
     (2, 3840, 2160, 1920, 1080),
@@ -169,9 +294,9 @@ STREAM_SHAPES = [
 
 @pytest.mark.parametrize("shape", STREAM_SHAPES, ids=lambda s: "L%d_%dx%d" % s[:3])
 def test_stream_variants_agree_with_oracle(shape):
-    """Every Lanczos streamer (block-shared symmetric at full and half lane width, accumulator ring,
-    per-wave symmetric), every prefetch depth, forced lane counts and band splits produce the
-    oracle's output."""
+    """Every Lanczos streamer (block-shared symmetric in XCD-aware and dispatch order, accumulator
+    ring, per-wave symmetric), every prefetch depth, forced lane counts and band splits produce
+    the oracle's output."""
     d, sw, sh, dw, dh = shape
     frames = _noise_batch(2, sw, sh, 300)
     frames[1, :, : sw // 5] = 255
@@ -182,6 +307,9 @@ def test_stream_variants_agree_with_oracle(shape):
                                       (2, 2, 40, 0), (3, 3, 0, 0), (3, 2, 0, 7), (3, 3, 41, 0), (3, 3, 0, 1)]:
         r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
         assert r.describe()["kernel"] == "lanczos_stream"
+        if variant == 3:  # block-shared streamer in plain dispatch order
+            variant = 0
+            r.set_option("xcd_order", 0)
         r.set_option("stream_variant", variant)
         r.set_option("prefetch", pd)
         r.set_option("lanes", lanes)
@@ -466,3 +594,80 @@ def test_sample_yuv420p_file_tool(tmp_path, m, iw, ih, ow, oh):
             dc = d[dx * dy + p * cd: dx * dy + (p + 1) * cd].reshape(dy // 2, dx // 2)
             exp = ol.run_oracle(method, degree, sx // 2, sy // 2, dx // 2, dy // 2, pxc, sc)
             assert (dc == exp).all(), (m, f, name)
+
+
+_DROPIN = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__))), "tests", "native", "_build", "dropin")
+
+
+@pytest.mark.parametrize("m,iw,ih,ow,oh", [("lanczos3", 640, 480, 320, 240), ("lanczos2", 1920, 1080, 1280, 720),
+                                           ("area", 640, 480, 160, 120), ("linear", 320, 240, 640, 480),
+                                           ("lanczos3", 401, 301, 200, 151)])
+def test_reference_sample_binary_on_gpu(tmp_path, m, iw, ih, ow, oh):
+    """The reference's own sample/resize_yuv420p.cpp, compiled UNCHANGED against include/libiqo +
+    libiqo_hip.so (tests/native/dropin.mk, built in the build container), run on the GPU: every
+    plane of its output file equals the Generic oracle (luma W x H at stride W+W%2, chroma
+    (W+W%2)/2 x (H+H%2)/2 with pxScale 2 for Lanczos, resize_yuv420p.cpp:66-163)."""
+    import os
+    import subprocess
+    exe = os.path.join(_DROPIN, "resize_yuv420p")
+    if not os.path.exists(exe):
+        pytest.skip("reference tools not built (build() builds them where /root/reference exists)")
+    sx, sy, dx, dy = iw + iw % 2, ih + ih % 2, ow + ow % 2, oh + oh % 2
+    nsrc, ndst = sx * sy * 3 // 2, dx * dy * 3 // 2
+    raw = ol.splitmix_bytes(nsrc, 21).astype(np.uint8)
+    fin, fout = tmp_path / "in.yuv", tmp_path / "out.yuv"
+    raw.tofile(str(fin))
+    r = subprocess.run([exe, "-m", m, "-i", str(fin), "-iw", str(iw), "-ih", str(ih), "-o", str(fout),
+                        "-ow", str(ow), "-oh", str(oh)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = np.fromfile(str(fout), dtype=np.uint8)
+    assert got.size == ndst
+    method = "lanczos" if m.startswith("lanczos") else m
+    degree = int(m[7]) if method == "lanczos" else 0
+    sY, dY = raw[:sx * sy].reshape(sy, sx), got[:dx * dy].reshape(dy, dx)
+    assert (dY[:oh, :ow] == ol.run_oracle(method, degree, iw, ih, ow, oh, 1, sY[:ih, :iw])).all()
+    cs, cd = sx * sy // 4, dx * dy // 4
+    for p in (0, 1):
+        sc = raw[sx * sy + p * cs: sx * sy + (p + 1) * cs].reshape(sy // 2, sx // 2)
+        dc = got[dx * dy + p * cd: dx * dy + (p + 1) * cd].reshape(dy // 2, dx // 2)
+        exp = ol.run_oracle(method, degree, sx // 2, sy // 2, dx // 2, dy // 2, 2 if method == "lanczos" else 1, sc)
+        assert (dc == exp).all(), (m, p)
+
+
+def test_reference_benchmark_binary_on_gpu():
+    """The reference's own benchmark/benchmark.cpp, compiled unchanged against the drop-in, runs
+    its 256-cycle timed loop (resizers constructed inside the loop) on the GPU backend."""
+    import os
+    import subprocess
+    exe = os.path.join(_DROPIN, "benchmark")
+    if not os.path.exists(exe):
+        pytest.skip("reference tools not built")
+    r = subprocess.run([exe, "-m", "lanczos3", "-iw", "3840", "-ih", "2160", "-ow", "1920", "-oh", "1080"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "elapsed time" in r.stdout and "ms/cycle" in r.stdout
+
+
+def test_concurrent_plans_from_host_threads(tmp_path):
+    """Distinct drop-in objects (Lanczos / Area / Linear, host pointers) used at the same time from
+    12 host threads, 3 rounds, a fresh object per thread and round: every concurrent output equals
+    the same job run alone (tests/native/threads_test.cpp), and every solo output equals the
+    Generic oracle."""
+    import glob
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(libiqo_amd.LIB_PATH), "build", "threads_test")
+    r = subprocess.run([exe, str(tmp_path), "12", "3"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    jobs = sorted(glob.glob(str(tmp_path / "*.src")))
+    assert len(jobs) == 12
+    for sp in jobs:
+        name = os.path.basename(sp)[:-4].split("_")
+        mi, d = int(name[1]), int(name[2])
+        sw, sh = map(int, name[3].split("x"))
+        dw, dh = map(int, name[4].split("x"))
+        src = np.fromfile(sp, np.uint8).reshape(sh, sw)
+        dst = np.fromfile(sp[:-4] + ".dst", np.uint8).reshape(dh, dw)
+        m = ("lanczos", "area", "linear")[mi]
+        assert (dst == ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)).all(), sp
