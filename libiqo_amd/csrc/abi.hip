@@ -475,6 +475,7 @@ iqo_amd::LinearDev linear_dev(const iqo_hip_plan *h)
     }
     l.dbg = h->debugFlags;
     l.prefetch = h->linPrefetch;
+    l.np = h->lanes;
     return l;
 }
 
@@ -708,7 +709,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->streamVariant = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "lanes")) {  // symmetric streamer producing lanes per wave (0 = auto)
+    if (!std::strcmp(key, "lanes")) {  // Lanczos / Linear streamers: producing lanes per wave (0 = auto)
         if (value < 0 || value > 62)
             return IQO_HIP_EINVAL;
         h->lanes = static_cast<int>(value);

@@ -1371,6 +1371,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+#ifdef IQO_VARIANT_DEBUG
+        if (dbg & 64) {  // timing experiment (wrong output): the row's bytes as 16 B per even lane
+            const int st16 = (lane & 1) ? 0x7ff00000 : stoff;
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o.x, o.y, o.x, o.y}, dstR, st16, (yy - a.io.dstRow0) * dstSt, 0);
+        } else
+#endif
         __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
@@ -2006,7 +2012,7 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
     // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
     const int lanes = g.srcW / 8;
     int wpr = (lanes + 61) / 62;
-    int np = (lanes + wpr - 1) / wpr;
+    int np = g.np > 0 ? min(g.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
     // nontemporal stores by default (variant builds: dbg 16 = plain stores, for A/B); 2 rows in
     // flight per wave measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)

@@ -88,6 +88,7 @@ struct LinearDev {
     uint32_t cx[2];
     int dbg;                     // variant builds only: 16 = plain (not nontemporal) stores
     int prefetch;                // source rows in flight per wave (2, 4, 8; 0 = default 2)
+    int np;                      // producing lanes per wave (0 = auto)
 };
 hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
                              hipStream_t s);
