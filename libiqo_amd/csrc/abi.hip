@@ -50,6 +50,10 @@ struct iqo_hip_plan {
     uint32_t *dTColCoef = nullptr;
     int32_t *dTColA = nullptr;
     int tileNQp = 0;
+    // general-ratio band walker over the same tables (option "walk" = 0 keeps tile_kernel)
+    iqo_amd::WalkTables wt;
+    bool useWalk = false;
+    int2 *dWSpans = nullptr;
 };
 
 namespace {
@@ -283,6 +287,7 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dTRowTap);
     (void)hipFree(h->dTColCoef);
     (void)hipFree(h->dTColA);
+    (void)hipFree(h->dWSpans);
     delete h;
 }
 
@@ -327,6 +332,15 @@ int upload_tile(iqo_hip_plan *h)
                 coefT[(static_cast<size_t>(p) * 4 + k) * nQp + Q] = in ? t.colCoef[static_cast<size_t>(x) * t.NP + p] : 0u;
         }
     h->tileNQp = nQp;
+    iqo_amd::build_walk_tables(h->p, t, &h->wt);
+    if (h->wt.ok) {
+        std::vector<int2> ws(h->wt.spans.size());
+        for (size_t i = 0; i < ws.size(); ++i)
+            ws[i] = make_int2(h->wt.spans[i].lo8, h->wt.spans[i].units);
+        const int rc = upload(&h->dWSpans, ws.data(), ws.size());
+        if (rc)
+            return rc;
+    }
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
     for (size_t y = 0; y < t.rows.size(); ++y)
@@ -505,6 +519,24 @@ iqo_amd::TileDev tile_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::WalkDev walk_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::WalkTables &w = h->wt;
+    iqo_amd::WalkDev d;
+    d.t = tile_dev(h);
+    d.CTW = w.CTW;
+    d.nTx = w.nTx;
+    d.wspans = h->dWSpans;
+    d.maxUnits = w.maxUnits;
+    d.R = w.R;
+    d.pitch = w.pitch;
+    d.chunks = w.chunks;
+    d.cpw = w.cpw;
+    d.maxNew = w.maxNew;
+    d.maxBand = w.maxBand;
+    return d;
+}
+
 iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
 {
     const Plan &p = h->p;
@@ -540,6 +572,9 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         kernel = IQO_KERNEL_GENERAL;
     if (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tt.ok && h->useTile)
         kernel = IQO_KERNEL_TILE;  // any alignment (the kernel adapts per frame)
+    // the band walker's LDS-DMA reads dwords: 4-byte aligned source frames and rows
+    if (kernel == IQO_KERNEL_TILE && h->wt.ok && h->useWalk && aligned(src, 4, srcSt, srcFrameSt))
+        kernel = IQO_KERNEL_WALK;
     return kernel;
 }
 
@@ -605,6 +640,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_linear_up2(linear_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_TILE)
             e = iqo_amd::launch_tile(tile_dev(h), io, rb, re, s);
+        else if (kernel == IQO_KERNEL_WALK)
+            e = iqo_amd::launch_walk(walk_dev(h), io, rb, re, h->bands, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -667,8 +704,9 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->phasesX = h->p.x.phases;
     d->phasesY = h->p.y.phases;
     d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL
-                                : (h->p.kernel == IQO_KERNEL_GENERAL && h->tt.ok && h->useTile ? IQO_KERNEL_TILE
-                                                                                              : h->p.kernel);
+                                : (h->p.kernel == IQO_KERNEL_GENERAL && h->tt.ok && h->useTile
+                                       ? (h->wt.ok && h->useWalk ? IQO_KERNEL_WALK : IQO_KERNEL_TILE)
+                                       : h->p.kernel);
     d->bandsPerFrame = h->bands;
     return IQO_HIP_OK;
 }
@@ -730,6 +768,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "tile")) {  // 0: shapes without a specialised kernel use general_kernel
         h->useTile = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "walk")) {  // 0: general ratios use tile_kernel instead of the band walker
+        h->useWalk = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "chunk_frames")) {  // frames per launch (0 = auto)
@@ -1230,7 +1272,10 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     if (h.p.kernel != IQO_KERNEL_GENERAL)
         return h.p.kernel;
     iqo_amd::build_tile_tables(h.p, &h.tt);
-    return h.tt.ok ? IQO_KERNEL_TILE : IQO_KERNEL_GENERAL;
+    if (!h.tt.ok)
+        return IQO_KERNEL_GENERAL;
+    iqo_amd::build_walk_tables(h.p, h.tt, &h.wt);
+    return h.wt.ok && h.useWalk ? IQO_KERNEL_WALK : IQO_KERNEL_TILE;
 }
 
 } // extern "C"

@@ -46,6 +46,20 @@ struct TileDev {
 };
 hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
 
+// --- general-ratio band walker: the tile tables walked band by band, each source row fetched
+// once per band into an LDS ring (LDS-DMA, dword lanes; 4-byte aligned source layouts).
+struct WalkDev {
+    TileDev t;                   // tables (t.spans / CT / TH unused)
+    int CTW, nTx;                // output columns per column tile, column tiles
+    const int2 *wspans;          // {lo8, units} per column tile; a unit = 4 work columns
+    int maxUnits;                // units of the widest tile
+    int R, pitch;                // ring rows (power of 2), ring row pitch (bytes, multiple of 256)
+    int chunks, cpw, maxNew;     // 256-B DMA chunks per ring row, chunks per wave, new rows per output row
+    int maxBand;                 // rows per band at most (tap records of a band live in LDS)
+};
+hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+size_t walk_lds_bytes(const WalkDev &w, int rowsPerBand);
+
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {
     int KY, KX, NY, NXP, offX;

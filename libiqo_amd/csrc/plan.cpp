@@ -856,4 +856,72 @@ void band_src_rows(const Plan &p, int r0, int r1, int *s0, int *s1)
     *s1 = hi;
 }
 
+// The walker's tables: the tile tables' rows and columns, its own column tiling and ring.
+void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w)
+{
+    *w = WalkTables();
+    if (!t.ok || t.nYp > 64 || p.srcW < 4 || t.NP > 8)
+        return;
+    // column tiles: as few as keep a tile within 1024 output columns (one quad per thread) and
+    // 2048 work columns (two 4-column units per thread)
+    int nT = (p.dstW + 1023) / 1024;
+    for (;; ++nT) {
+        const int ctw = ((p.dstW + nT - 1) / nT + 3) & ~3;
+        int maxU = 0;
+        std::vector<WalkSpan> sp(static_cast<size_t>(nT));
+        bool ok = true;
+        for (int k = 0; k < nT && ok; ++k) {
+            const int x0 = k * ctw, x1 = std::min(p.dstW, x0 + ctw);
+            if (x0 >= x1) {
+                ok = false;
+                break;
+            }
+            int lo = 1 << 30, hi = -(1 << 30);
+            for (int x = x0; x < x1; ++x) {
+                lo = std::min(lo, t.cols[static_cast<size_t>(x)].a);
+                hi = std::max(hi, t.cols[static_cast<size_t>(x)].a + 2 * t.NP);
+            }
+            const int lo8 = lo & ~7;
+            const int units = (hi - lo8 + 3) / 4;
+            sp[static_cast<size_t>(k)] = WalkSpan{lo8, units};
+            maxU = std::max(maxU, units);
+        }
+        if (!ok || nT > 64)
+            return;
+        if (maxU > 512)
+            continue;
+        w->CTW = ctw;
+        w->nTx = nT;
+        w->spans = sp;
+        w->maxUnits = maxU;
+        break;
+    }
+    // ring: rows spanned by any output row and the kWalkPrefetch rows after it
+    int need = 1, maxNew = 1;
+    for (int y = 0; y < p.dstH; ++y) {
+        const int y2 = std::min(y + kWalkPrefetch, p.dstH - 1);
+        need = std::max(need, t.rows[static_cast<size_t>(y2)].hi - t.rows[static_cast<size_t>(y)].lo + 1);
+        if (y > 0)
+            maxNew = std::max(maxNew, t.rows[static_cast<size_t>(y)].hi - t.rows[static_cast<size_t>(y - 1)].hi);
+    }
+    int R = 1;
+    while (R < need)
+        R *= 2;
+    w->R = R;
+    w->pitch = (4 * w->maxUnits + 8 + 255) & ~255;
+    w->chunks = w->pitch / 256;
+    w->cpw = (w->chunks + 3) / 4;
+    w->maxNew = maxNew;
+    // DMAs per wave per output row stay small enough for the constant waits (kernels.hip)
+    if (maxNew * w->cpw > 8)
+        return;
+    // bands: tap records (8 B per tap) and row records (16 B) of a band in at most 24 KiB
+    w->maxBand = std::max(1, std::min(512, 24 * 1024 / (8 * t.nYp + 16)));
+    const size_t lds = static_cast<size_t>(R) * w->pitch + 2 * 8 * static_cast<size_t>(w->maxUnits) +
+                       static_cast<size_t>(w->maxBand) * (8 * t.nYp + 16) + 256;
+    if (lds > 64 * 1024)
+        return;
+    w->ok = true;
+}
+
 } // namespace iqo_amd

@@ -147,6 +147,25 @@ size_t tile_lds_bytes(const Plan &p, const TileTables &t, int TH);
 int tile_src_rows(const Plan &p, const TileTables &t, int TH);
 bool tile_set_rows(const Plan &p, TileTables *t, int TH);
 
+// Geometry of the general-ratio band walker (kernels.hip walk_kernel) over the tile tables:
+// column tiles of CTW output columns (at most 1024: one quad of 4 columns per thread), each with
+// its work-column span in 4-column units, and an LDS ring of R source rows.
+struct WalkSpan {
+    int32_t lo8, units;           // first work column (multiple of 8), 4-column units
+};
+struct WalkTables {
+    bool ok = false;
+    int CTW = 0, nTx = 0;
+    std::vector<WalkSpan> spans;  // nTx
+    int maxUnits = 0;             // at most 512 (two units per thread)
+    int R = 0, pitch = 0;         // ring rows (power of 2), ring row pitch (multiple of 256)
+    int chunks = 0, cpw = 0;      // 256-B DMA chunks per row, per wave (4 waves)
+    int maxNew = 0;               // most source rows first needed by one output row
+    int maxBand = 0;              // rows per band at most (tap records of a band in LDS)
+};
+constexpr int kWalkPrefetch = 3;  // output rows of DMA look-ahead (kernels.hip kWalkD)
+void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w);
+
 // Build the full plan.  Returns false (with *err) for invalid arguments.
 bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                 size_t pxScale, Plan *out, std::string *err);

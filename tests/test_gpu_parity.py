@@ -370,21 +370,43 @@ TILE_SHAPES = [
 
 @pytest.mark.parametrize("cfg", TILE_SHAPES, ids=lambda c: "%s%d_%dx%d_%dx%d" % c[:6])
 def test_tile_streamer_matches_oracle(cfg):
-    """The separable tile kernel (shapes without a specialised kernel) equals the oracle with
-    aligned and byte-aligned sources and destinations (8-byte, 12-byte-shifted and single-byte
-    loads; dword and byte stores), and equals general_kernel (plan option tile = 0) on the same
-    batch."""
+    """General ratios (shapes without a specialised kernel): the separable tile kernel (the
+    default; every misaligned layout: 8-byte, 12-byte-shifted and single-byte loads; dword and
+    byte stores), the band walker (plan option walk = 1 on 4-byte aligned sources; several band
+    splits and a padded stride) equal the oracle, and general_kernel (tile = 0) on the same batch."""
     m, d, sw, sh, dw, dh, px = cfg
     frames = _noise_batch(2, sw, sh, 1100)
     frames[1, :, : sw // 3] = 255
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
+    t = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    assert r.describe()["kernel"] == "tile"
+    r.set_option("walk", 1)
+    kern = r.describe()["kernel"]
+    assert kern in ("walk", "tile")
     src = torch.from_numpy(frames).to(DEV)
-    out = r.resize_tensor(src).cpu().numpy()
-    for f in range(2):
-        bad = np.argwhere(out[f] != exp[f])
-        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    for rr in (r, t):
+        out = rr.resize_tensor(src).cpu().numpy()
+        for f in range(2):
+            bad = np.argwhere(out[f] != exp[f])
+            assert bad.size == 0, (cfg, rr.describe()["kernel"], f, bad[:4].tolist())
+    if kern == "walk":
+        for bands in (1, 3, 7, dh):
+            w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+            w.set_option("walk", 1)
+            w.set_option("bands", bands)
+            out = w.resize_tensor(src).cpu().numpy()
+            for f in range(2):
+                bad = np.argwhere(out[f] != exp[f])
+                assert bad.size == 0, (cfg, "walk bands", bands, f, bad[:4].tolist())
+        sst = (sw + 7) & ~3  # 4-byte aligned padded stride: the walker again
+        pbuf = torch.zeros((2, sh, sst), dtype=torch.uint8, device=DEV)
+        pbuf[:, :, :sw] = src
+        dbuf = torch.zeros((2, dh, dw + 3), dtype=torch.uint8, device=DEV)
+        r.resize_device(2, sst, sh * sst, pbuf.data_ptr(), dw + 3, dh * (dw + 3), dbuf.data_ptr())
+        got = dbuf[:, :, :dw].cpu().numpy()
+        for f in range(2):
+            assert (got[f] == exp[f]).all(), (cfg, "walk padded", f)
     # misaligned base (byte loads), padded strides
     sst = sw + 3
     sbuf = torch.zeros(sh * sst + 64, dtype=torch.uint8, device=DEV)
