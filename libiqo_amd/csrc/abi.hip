@@ -53,7 +53,10 @@ struct iqo_hip_plan {
     // general-ratio band walker over the same tables (option "walk" = 0 keeps tile_kernel)
     iqo_amd::WalkTables wt;
     bool useWalk = false;
-    int2 *dWSpans = nullptr;
+    int4 *dWSpans = nullptr;
+    int4 *dWSegs = nullptr;
+    uint32_t *dWRowTap = nullptr;
+    int4 *dWRows = nullptr;
 };
 
 namespace {
@@ -288,6 +291,9 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dTColCoef);
     (void)hipFree(h->dTColA);
     (void)hipFree(h->dWSpans);
+    (void)hipFree(h->dWRowTap);
+    (void)hipFree(h->dWRows);
+    (void)hipFree(h->dWSegs);
     delete h;
 }
 
@@ -334,10 +340,26 @@ int upload_tile(iqo_hip_plan *h)
     h->tileNQp = nQp;
     iqo_amd::build_walk_tables(h->p, t, &h->wt);
     if (h->wt.ok) {
-        std::vector<int2> ws(h->wt.spans.size());
+        std::vector<int4> ws(h->wt.spans.size());
         for (size_t i = 0; i < ws.size(); ++i)
-            ws[i] = make_int2(h->wt.spans[i].lo8, h->wt.spans[i].units);
-        const int rc = upload(&h->dWSpans, ws.data(), ws.size());
+            ws[i] = make_int4(h->wt.spans[i].lo8, h->wt.spans[i].units, h->wt.spans[i].interior, 0);
+        std::vector<int4> sg(2 * h->wt.segs.size());
+        for (size_t i = 0; i < h->wt.segs.size(); ++i) {
+            const iqo_amd::WalkSeg &g = h->wt.segs[i];
+            sg[2 * i] = make_int4(g.first, g.slotOff, g.border, g.firstD);
+            sg[2 * i + 1] = make_int4(static_cast<int>(g.yM), g.yS, g.yNeg, 0);
+        }
+        std::vector<int4> wr(h->wt.rows.size());
+        for (size_t i = 0; i < wr.size(); ++i)
+            wr[i] = make_int4(h->wt.rows[i].lo, h->wt.rows[i].hi, h->wt.rows[i].hiSlot, h->wt.rows[i].deno);
+        const std::vector<uint32_t> &wt = h->wt.rowTap;
+        int rc = upload(&h->dWSpans, ws.data(), ws.size());
+        if (!rc)
+            rc = upload(&h->dWRows, wr.data(), wr.size());
+        if (!rc)
+            rc = upload(&h->dWRowTap, wt.data(), wt.size());
+        if (!rc)
+            rc = upload(&h->dWSegs, sg.data(), sg.size());
         if (rc)
             return rc;
     }
@@ -524,16 +546,15 @@ iqo_amd::WalkDev walk_dev(const iqo_hip_plan *h)
     const iqo_amd::WalkTables &w = h->wt;
     iqo_amd::WalkDev d;
     d.t = tile_dev(h);
-    d.CTW = w.CTW;
-    d.nTx = w.nTx;
-    d.wspans = h->dWSpans;
-    d.maxUnits = w.maxUnits;
+    d.nS = w.nS;
+    d.spans = h->dWSpans;
+    d.NV = w.NV;
     d.R = w.R;
     d.pitch = w.pitch;
-    d.chunks = w.chunks;
-    d.cpw = w.cpw;
-    d.maxNew = w.maxNew;
-    d.maxBand = w.maxBand;
+    d.waveBytes = static_cast<int>(w.waveBytes);
+    d.rowTap = h->dWRowTap;
+    d.rows = h->dWRows;
+    d.segs = h->dWSegs;
     return d;
 }
 
@@ -572,7 +593,7 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         kernel = IQO_KERNEL_GENERAL;
     if (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tt.ok && h->useTile)
         kernel = IQO_KERNEL_TILE;  // any alignment (the kernel adapts per frame)
-    // the band walker's LDS-DMA reads dwords: 4-byte aligned source frames and rows
+    // the wave walker loads aligned dwords: 4-byte aligned source frames and rows
     if (kernel == IQO_KERNEL_TILE && h->wt.ok && h->useWalk && aligned(src, 4, srcSt, srcFrameSt))
         kernel = IQO_KERNEL_WALK;
     return kernel;

@@ -15,6 +15,7 @@
 #include <climits>
 #include <cstdint>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 #include <utility>
 
@@ -1414,97 +1415,80 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WA
 }
 
 
-// ================================================================ general-ratio band walker
+// ================================================================ general-ratio wave walker
 //
 // The shapes of tile_kernel (multi-phase ratios, Lanczos upscaling and degrees 1-9, non-integer
-// Area, Linear other than 2x) with tile_kernel's tables and arithmetic, but laid out like the
-// streamers: a WORKGROUP walks a band of output rows of one column tile of one frame top to
-// bottom, and every source row of the band lands ONCE in an LDS ring (LDS-DMA, 4 bytes per lane,
-// chunk c of a row by wave c mod 4) kWalkD output rows before it is first needed.  tile_kernel
-// stages each tile's rows + halo and stalls on that burst; here the halo is read once per band
-// and the loads of row y+kWalkD overlap the arithmetic of row y.
+// Area, Linear other than 2x) with tile_kernel's arithmetic, laid out like the streamers: every
+// WAVE owns a strip of 256 output columns (4 per lane, one dword store) of one band of output
+// rows of one frame and walks it top to bottom.  No barrier anywhere: a wave only ever reads the
+// LDS it wrote itself, so the waves of a workgroup (and of a CU) never wait for each other.
 //
-// Per output row ("segment") s of the band, one barrier:
-//   wait for this wave's DMAs of segment s-kWalkD (counted vmcnt) -> s_barrier ->
-//   issue the DMAs of the rows first needed by row s+kWalkD ->
-//   horizontal pass of row s-1 from work buffer (s-1)&1 (4 outputs per thread, one store) ->
-//   vertical pass of row s into work buffer s&1 (4-column units: per tap one 8-byte LDS read,
-//   two v_perm -- per-lane selectors that also replicate the edge columns -- and two v_pk_mad_u16).
-// Every wave issues exactly NDMA = maxNew * cpw DMAs (unused ones land in a sink) and one store
-// per segment, so the waits are constants of the plan.  The ring holds R >= (rows spanned by
-// rows s .. s+kWalkD) rows, so a DMA never overwrites a row still being read.
-
-constexpr int kWalkD = 3;  // prefetch distance in output rows
+// Per output row s of the band ("segment"):
+//   1. widen the source rows first needed by row s, (hi(s-1), hi(s)] -- loaded two segments
+//      earlier into VGPRs, one aligned dword per 4-column unit -- to u16 with two v_perm per unit
+//      (per-lane selectors also replicate the edge columns) and write them to the wave's LDS
+//      ring (slot = source row % R, R = the widest row window);
+//   2. issue the dword loads of the rows of row s+2 into the registers just freed;
+//   3. vertical pass: per tap one aligned 8-byte LDS read and two v_pk_mad_u16 per unit, tap
+//      records (coefficient splat, ring byte offset) read through the scalar cache;
+//   4. horizontal pass from the wave's work row: NP dword reads and NP v_dot2 per output, one
+//      dword store per lane.
+// The source is read once per band (plus the first row's window), the output written once.
 
 struct WalkArgs {
     WalkDev w;
     Io io;
     int rowBegin, rowEnd, rowsPerBand, bands;
     int srcBytes, dstBytes;
-    unsigned nWG;     // nTx * bands * frames (flat grid)
-    int ndma;         // DMA instructions per wave per segment (maxNew * cpw)
+    unsigned nWaves;  // nS * bands * frames
 };
 
-// 4 bytes per lane: LDS [lds + 4*lane] <- buffer[voff + soff] (voff out of range: no traffic, 0)
-__device__ __forceinline__ void dma_dword(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff)
+constexpr int kWalkD = 4;  // load look-ahead in output rows (plan.hpp kWalkPrefetch)
+
+// (-lo, -hi) of two int16 halves
+__device__ __forceinline__ uint32_t pk_neg16(uint32_t w)
 {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                 "buffer_load_dword %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
-                 : "memory");
+    return ((0u - (w & 0xffffu)) & 0xffffu) | ((0u - (w >> 16)) << 16);
 }
 
-// s_waitcnt vmcnt(n) for a uniform runtime n (the immediate must be a constant)
-__device__ __forceinline__ void wait_vmcnt_rt(int n)
+// Wave-uniform reads of read-only tables through the scalar cache (s_load).
+__device__ __forceinline__ int sld(const void *p, int i)
 {
-    switch (n) {
-#define IQO_W(k) case k: wait_vmcnt<k>(); break;
-        IQO_W(0) IQO_W(1) IQO_W(2) IQO_W(3) IQO_W(4) IQO_W(5) IQO_W(6) IQO_W(7) IQO_W(8) IQO_W(9)
-        IQO_W(10) IQO_W(11) IQO_W(12) IQO_W(13) IQO_W(14) IQO_W(15) IQO_W(16) IQO_W(17) IQO_W(18)
-        IQO_W(19) IQO_W(20) IQO_W(21) IQO_W(22) IQO_W(23) IQO_W(24) IQO_W(25) IQO_W(26) IQO_W(27)
-        IQO_W(28) IQO_W(29) IQO_W(30)
-#undef IQO_W
-    default: wait_vmcnt<0>(); break;
-    }
+    return ((const __attribute__((address_space(4))) int *)(p))[i];
 }
+__device__ __forceinline__ int4 sload(const int4 *p) { return make_int4(sld(p, 0), sld(p, 1), sld(p, 2), sld(p, 3)); }
 
-template <int NP, bool LZ>
+template <int NP, int VY, int NV, bool LZ>
 __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a)
 {
+    // VY: vertical taps, 2 * NP or 2 * NP - 2 (plan.cpp build_walk_tables)
+    constexpr int OOB = 0x7ff00000;      // buffer offset past every range: no traffic, reads 0
     extern __shared__ __attribute__((aligned(16))) uint8_t wl[];
     const WalkDev &W = a.w;
     const TileDev &t = W.t;
-    const int tid = static_cast<int>(threadIdx.x), lane = tid & 63;
-    const int wib = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // flat id -> (column tile, band, frame), XCD-spread: the tiles and bands of a frame run on one
-    // XCD, so the halo rows neighbouring bands share hit that XCD's L2
-    const unsigned lg = xcd_spread(blockIdx.x, a.nWG);
-    const int tileX = static_cast<int>(lg % static_cast<unsigned>(W.nTx));
-    const unsigned rest = lg / static_cast<unsigned>(W.nTx);
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    // flat wave id -> (strip, band, frame); XCD-spread by workgroup, so neighbouring strips and
+    // bands (which share halo rows and columns) run on one XCD's L2
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;  // whole wave; the kernel has no barrier
+    const int strip = static_cast<int>(gw % static_cast<unsigned>(W.nS));
+    const unsigned rest = gw / static_cast<unsigned>(W.nS);
     const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
     const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
     const int y0 = a.rowBegin + band * a.rowsPerBand;
     const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
     if (y0 >= y1)
-        return;  // whole workgroup
-    const int nRows = y1 - y0;
-    const int2 sp = W.wspans[tileX];
+        return;
+    const int4 sp = sload(W.spans + strip);  // {lo8, units, interior, 0}
     const int lo8 = sp.x, units = sp.y;
-    const int R = W.R, pitch = W.pitch, nYp = t.nYp;
-    const int srcW = t.srcW;
-
-    // LDS: ring [R][pitch] | work [2][maxUnits][8 B] | tap records [nRows][nYp] (coef, ring
-    // offset) | row records [nRows] (lo, hi, deno) | DMA sink [256 B]
-    const uint32_t ldsBase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
-        (__attribute__((address_space(3))) uint8_t *)wl));
-    const int workOff = R * pitch, workBytes = W.maxUnits * 8;
-    const int tapOff = workOff + 2 * workBytes;
-    const int recOff = tapOff + nRows * nYp * 8;
-    const uint32_t sinkLds = ldsBase + static_cast<uint32_t>(recOff + nRows * 16);
-    uint2 *const taps = reinterpret_cast<uint2 *>(wl + tapOff);
-    int4 *const recs = reinterpret_cast<int4 *>(wl + recOff);
+    const int R = W.R, pitch = W.pitch, srcW = t.srcW;
+    const int ringBytes = R * pitch;
+    // LDS per wave: ring [R][pitch] | work row [512 NV] | sink [512] (NV = 2: idle lanes' writes)
+    uint8_t *const ring = wl + wib * W.waveBytes;
+    uint8_t *const work = ring + ringBytes;
+    const int sinkOff = ringBytes + 512 * NV;
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
@@ -1512,33 +1496,20 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a)
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
-    const int srcRow0 = a.io.srcRow0;
+    const int srcRow0 = a.io.srcRow0, srcLast = a.io.srcRowEnd - 1;
     const bool dstA4 = !(reinterpret_cast<uintptr_t>(dstFrame) & 3) && !(a.io.dstSt & 3);
+    // interior strip: 256 columns, no masked border column, aligned rows: one plain dword store
+    const bool interior = sp.z != 0 && dstA4;
 
-    // tap records of the band: (coefficient splat, ring offset of the clamped source row)
-    for (int i = tid; i < nRows * nYp; i += 256) {
-        const uint2 rt = t.rowTap[static_cast<int64_t>(y0) * nYp + i];
-        taps[i] = make_uint2(rt.x, static_cast<uint32_t>((static_cast<int>(rt.y) & (R - 1)) * pitch));
-    }
-    for (int i = tid; i < nRows; i += 256) {
-        const int4 r = t.rows[y0 + i];
-        recs[i] = make_int4(r.y, r.z, r.w, 0);
-    }
-    // row windows [lo, hi] (monotone in the row): rows first needed by row y are (hi(y-1), hi(y)];
-    // read from the LDS copy (uniform), never by a vector load inside the DMA pipeline
-    auto rlo = [&](int y) { return __builtin_amdgcn_readfirstlane(recs[y - y0].x); };
-    auto rhi = [&](int y) { return __builtin_amdgcn_readfirstlane(recs[y - y0].y); };
-
-    // horizontal ownership: output columns x0 .. x0+3 of the tile, coefficient pairs in VGPRs
-    const int nQ = (W.CTW + 3) >> 2;
-    const int x0 = tileX * W.CTW + 4 * tid;
-    const bool hq = tid < nQ && x0 < t.dstW;
+    // horizontal ownership: output columns x0 .. x0+3, coefficient pairs in VGPRs
+    const int x0 = strip * 256 + 4 * lane;
+    const bool hq = x0 < t.dstW;
     const int Q = min(x0, t.dstW - 1) >> 2;
     uint32_t cf[4][NP];
     int woff[4], DL[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        woff[k] = hq ? (t.colA[k * t.nQp + Q] - lo8) >> 1 : 0;
+        woff[k] = hq ? 4 * ((t.colA[k * t.nQp + Q] - lo8) >> 1) : 0;  // byte offset in the work row
         DL[k] = (LZ && hq && x0 + k < t.dstW) ? t.cols[x0 + k].y : 0;
 #pragma unroll
         for (int p = 0; p < NP; ++p)
@@ -1549,163 +1520,217 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a)
     for (int k = 0; k < 4; ++k)
         anyD |= DL[k] != 0;
 
-    // vertical ownership: units u = tid, tid + 256, ... (at most 2 per thread); per-lane byte
-    // selectors into the 8 aligned ring bytes at A, replicating columns < 0 and >= srcW
-    int A[2];
-    uint32_t s01[2], s23[2];
+    // widening ownership: units u = lane + 64 m, source columns lo8 + 4u .. +3 clamped to
+    // [0, srcW): all four lie in ONE aligned dword (lo8 is a multiple of 8), byte selectors pick
+    // them.  Idle lanes (u >= units) load nothing and widen into the sink.
+    int gcol[NV], wOff[NV];
+    uint32_t sLo[NV], sHi[NV];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
-        const int u = tid + 256 * m;
+    for (int m = 0; m < NV; ++m) {
+        const int u = lane + 64 * m;
+        const bool uv = u < units;
         const int cb = lo8 + 4 * u;
-        const int lo = min(max(cb, 0), srcW - 1);
-        A[m] = (lo - lo8) & ~3;
+        const int g = min(max(cb, 0), srcW - 1) & ~3;
+        gcol[m] = uv ? g : OOB;
+        wOff[m] = uv ? 8 * u : 1 << 20;  // idle: past any slot, clamped into the sink below
         int idx[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            idx[k] = min(max(cb + k, 0), srcW - 1) - (lo8 + A[m]);
-        s01[m] = static_cast<uint32_t>(idx[0] | (idx[1] << 16)) | 0x0c000c00u;
-        s23[m] = static_cast<uint32_t>(idx[2] | (idx[3] << 16)) | 0x0c000c00u;
+            idx[k] = min(max(cb + k, 0), srcW - 1) - g;
+        sLo[m] = static_cast<uint32_t>(idx[0] | (idx[1] << 16)) | 0x0c000c00u;
+        sHi[m] = static_cast<uint32_t>(idx[2] | (idx[3] << 16)) | 0x0c000c00u;
     }
-
-    // DMA of ring row r (chunks c = wib + 4j): lanes outside [0, srcW) read nothing
-    const int ndma = a.ndma, maxNew = W.maxNew;
-    auto dma_row = [&](int r, bool valid) {
-        for (int j = 0; j < W.cpw; ++j) {
-            const int c = wib + 4 * j;
-            const bool real = valid && c < W.chunks;
-            const int col = lo8 + 256 * c + 4 * lane;
-            const int v = (real && col >= 0 && col < srcW) ? col : 0x7ff00000;
-            const uint32_t d = real ? ldsBase + static_cast<uint32_t>((r & (R - 1)) * pitch + 256 * c) : sinkLds;
-            dma_dword(d, v, srcR, real ? (r - srcRow0) * srcSt : 0);
-        }
+    const int laneOff = 8 * lane;
+    // NV = 1: the pitch is 512 and idle lanes widen their zeros into their own slot bytes;
+    // NV = 2: every m = 0 lane is busy, idle m = 1 lanes widen into the sink
+    auto widen = [&](int slotOff, uint32_t v, int m) {
+        const int o = m == 0 ? slotOff + laneOff : min(slotOff + wOff[m], sinkOff + laneOff);
+        *reinterpret_cast<uint2 *>(ring + o) =
+            make_uint2(__builtin_amdgcn_perm(0u, v, sLo[m]), __builtin_amdgcn_perm(0u, v, sHi[m]));
     };
-    // one segment's DMA group: rows (from, to] (at most maxNew), then padding into the sink
-    auto dma_group = [&](int from, int to) {
-        for (int j = 0; j < maxNew; ++j)
-            dma_row(from + 1 + j, from + 1 + j <= to);
-    };
-    auto dropped_store = [&]() { __builtin_amdgcn_raw_buffer_store_b32(0u, dstR, 0x7ff00000, 0x7ff00000, 0); };
+    auto row_off = [&](int r) { return (min(r, srcLast) - srcRow0) * srcSt; };
 
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // tap / row records staged
-    // the column tables are consumed here, so the compiler's own wait for them sits before the
-    // DMA pipeline and not at their first use inside it (which would drain every prefetch)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        asm volatile("" ::"v"(woff[k]), "v"(DL[k]));
-#pragma unroll
-        for (int p = 0; p < NP; ++p)
-            asm volatile("" ::"v"(cf[k][p]));
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-
-    // prologue: the window of row y0, then the new rows of rows y0+1 .. y0+kWalkD-1, one group each
+    // the window of row y0, 8 rows per batch
     {
-        int r = rlo(y0) - 1;
-        const int h0 = rhi(y0);
-        do {
-            const int to = min(r + maxNew, h0);
-            dma_group(r, to);
-            dropped_store();
-            r = to;
-        } while (r < h0);
-        for (int j = 1; j < kWalkD; ++j) {
-            const int y = y0 + j;
-            if (y < y1)
-                dma_group(rhi(y - 1), rhi(y));
-            else
-                dma_group(0, -1);
-            dropped_store();
+        const int4 w0 = sload(W.rows + y0);  // {lo, hi, hi % R, deno}
+        for (int r = w0.x; r <= w0.y; r += 8) {
+            uint32_t v[8][NV];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int m = 0; m < NV; ++m)
+                    v[j][m] = __builtin_amdgcn_raw_buffer_load_b32(srcR, r + j <= w0.y ? gcol[m] : OOB, row_off(r + j), 0);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (r + j <= w0.y) {
+                    const int slotOff = ((r + j) % R) * pitch;
+#pragma unroll
+                    for (int m = 0; m < NV; ++m)
+                        widen(slotOff, v[j][m], m);
+                }
         }
     }
-    const int waitN = (kWalkD - 1) * (ndma + 1) + 1;
 
-    for (int s = y0; s <= y1; ++s) {
-        // this wave's rows of row s have landed; the barrier publishes everybody's and retires
-        // the reads of the ring slots and work buffer reused below
-        wait_vmcnt_rt(waitN);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        {
-            const int y = s + kWalkD;
-            if (y < y1)
-                dma_group(rhi(y - 1), rhi(y));
-            else
-                dma_group(0, -1);
+    // Segment s (plan.cpp WalkSeg) widens rows first(s) .. first(s)+NV-1 -- loaded during segment
+    // s-D -- and loads rows first(s+D) .. +NV-1 into the registers it freed: NV x NV dword loads
+    // per segment, no predicate.  Rows past hi(s) are written early; the ring holds the widest
+    // window + NV rows, so they never overwrite a live row.
+    constexpr int D = kWalkD;
+    auto issue = [&](int first, uint32_t (&b)[NV][NV]) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int soff = row_off(first + j);
+#pragma unroll
+            for (int m = 0; m < NV; ++m)
+                b[j][m] = __builtin_amdgcn_raw_buffer_load_b32(srcR, gcol[m], soff, 0);
         }
-        // horizontal pass of row s-1
-        if (s > y0) {
-            const uint32_t *w = reinterpret_cast<const uint32_t *>(wl + workOff + ((s - 1) & 1) * workBytes);
-            uint32_t bytes[4];
+    };
+    // tap records of row y: {(c, c) splat, ring byte offset} per tap
+    auto load_rec = [&](int y, uint32_t (&rc)[VY], uint32_t (&ro)[VY]) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                int sum = LZ ? (1 << 19) : (1 << 22);
+        for (int i = 0; i < VY; ++i) {
+            rc[i] = static_cast<uint32_t>(sld(W.rowTap, 2 * (y * VY + i)));
+            ro[i] = static_cast<uint32_t>(sld(W.rowTap, 2 * (y * VY + i) + 1));
+        }
+    };
+    // s_waitcnt lgkmcnt(0) the compiler's waitcnt pass sees (so it adds no per-use waits after it)
+    auto lgkm0 = [] { __builtin_amdgcn_s_waitcnt(0xc07f); };
+
+    // Segment s: g = {first(s), ring offset of first(s), border row, first(s+D)} (loaded by the
+    // previous segment)
+    auto segment = [&](auto edge, int s, int4 &g, uint32_t (&b)[NV][NV]) {
+        constexpr bool EDGE = decltype(edge)::value;
+        const int4 gs = g;
+        g = sload(W.segs + 2 * (s + 1));  // the next segment's record (the table is padded)
+        uint32_t rc[VY], ro[VY];
+        load_rec(s, rc, ro);
+        // 1. rows first(s) .. first(s)+NV-1 into the ring
+        {
+            int off = gs.y;
 #pragma unroll
-                for (int p = 0; p < NP; ++p)
-                    sum = LZ ? sdot2(w[woff[k] + p], cf[k][p], sum)
-                             : static_cast<int>(udot2(w[woff[k] + p], cf[k][p], static_cast<uint32_t>(sum)));
-                if (LZ) {
-                    int v = sum >> 20;
-                    if (anyD && DL[k] != 0)
-                        v = static_cast<int16_t>(exact_div(sum, DL[k]));
-                    bytes[k] = static_cast<uint32_t>(min(max(v, 0), 255));
-                } else {
-                    bytes[k] = min((static_cast<uint32_t>(sum) >> 23) & 0xffffu, 255u);
+            for (int j = 0; j < NV; ++j) {
+                if (j > 0) {
+                    off += pitch;
+                    off = off >= ringBytes ? off - ringBytes : off;
                 }
+#pragma unroll
+                for (int m = 0; m < NV; ++m)
+                    widen(off, b[j][m], m);
             }
-            const int off = (s - 1 - a.io.dstRow0) * dstSt + x0;
-            const bool whole = hq && dstA4 && x0 + 4 <= t.dstW;
-            const uint32_t o = opaque(bytes[0] | (bytes[1] << 8)) | (bytes[2] << 16) | (bytes[3] << 24);
-            __builtin_amdgcn_raw_buffer_store_b32(o, dstR, whole ? off : 0x7ff00000, 0, 0);
-            if (hq && !whole) {  // frame edge / unaligned: bytes (extra vm ops only make waits stricter)
+        }
+        // 2. the rows of segment s+D into the registers just freed
+        issue(gs.w, b);
+        // 3. vertical pass of row s into the work row (idle lanes compute on whatever they read)
+#pragma unroll
+        for (int m = 0; m < NV; ++m) {
+            const uint8_t *col = ring + laneOff + 512 * m;
+            // every tap's LDS read in flight, then one wait: left to itself the scheduler trades
+            // this ILP for registers and serialises VY LDS round trips
+            uint2 v[VY];
+#pragma unroll
+            for (int i = 0; i < VY; ++i)
+                v[i] = *reinterpret_cast<const uint2 *>(col + ro[i]);
+            lgkm0();
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t acc0 = 0, acc1 = 0;
+#pragma unroll
+            for (int i = 0; i < VY; ++i) {
+                acc0 = pk_mad(v[i].x, rc[i], acc0);
+                acc1 = pk_mad(v[i].y, rc[i], acc1);
+            }
+            if (LZ && gs.z != 0) {  // masked + renormalised border row: int16(nume * 64 / deno)
+                const int4 mg = sload(W.segs + 2 * s + 1);  // {yM, yS, yNeg, 0}
+                if (mg.z) {  // n / -d = -n / d
+                    acc0 = pk_neg16(acc0);
+                    acc1 = pk_neg16(acc1);
+                }
+                acc0 = ydiv2(acc0, static_cast<uint32_t>(mg.x), mg.y);
+                acc1 = ydiv2(acc1, static_cast<uint32_t>(mg.x), mg.y);
+            }
+            *reinterpret_cast<uint2 *>(work + laneOff + 512 * m) = make_uint2(acc0, acc1);
+        }
+        // 4. horizontal pass of row s: every LDS read, one wait, then the dot products
+        uint32_t wv[4][NP];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                wv[k][p] = *reinterpret_cast<const uint32_t *>(work + woff[k] + 4 * p);
+        lgkm0();
+        __builtin_amdgcn_sched_barrier(0);
+        int sum[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sum[k] = LZ ? (1 << 19) : (1 << 22);
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+                sum[k] = LZ ? sdot2(wv[k][p], cf[k][p], sum[k])
+                            : static_cast<int>(udot2(wv[k][p], cf[k][p], static_cast<uint32_t>(sum[k])));
+        }
+        const int off = (s - a.io.dstRow0) * dstSt + x0;
+        if (LZ && !EDGE) {
+            // main columns: sat_u8(sum >> 20) packed by v_ashr_pk_u8_i32
+            __builtin_amdgcn_raw_buffer_store_b32(pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]), dstR, off, 0, 0);
+            return;
+        }
+        uint32_t bytes[4];
+        if (LZ) {
+            int v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[k] = sum[k] >> 20;
+            if (anyD) {  // masked + renormalised edge columns (rare lanes)
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
-                    if (x0 + k < t.dstW)
-                        __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(bytes[k]), dstR, off + k, 0, 0);
+                    if (DL[k] != 0)
+                        v[k] = static_cast<int16_t>(exact_div(sum[k], DL[k]));
             }
-        } else {
-            dropped_store();
-        }
-        // vertical pass of row s
-        if (s < y1) {
-            const uint2 *tp = taps + (s - y0) * nYp;
-            const int deno = __builtin_amdgcn_readfirstlane(recs[s - y0].z);
-            uint32_t *wout = reinterpret_cast<uint32_t *>(wl + workOff + (s & 1) * workBytes);
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                const int u = tid + 256 * m;
-                if (u < units) {
-                    const uint8_t *colL = wl + A[m];
-                    uint32_t acc0 = 0, acc1 = 0;
-                    for (int i = 0; i < nYp; i += 2) {
-                        const uint4 c2 = *reinterpret_cast<const uint4 *>(tp + i);  // (coef, offset) x 2
-                        // two dword reads: A is only 4-byte aligned, and an 8-byte LDS read off
-                        // its natural alignment is replayed (MI355X_MICROARCH.md, LDS)
-                        const uint32_t *p0 = reinterpret_cast<const uint32_t *>(colL + c2.y);
-                        const uint32_t *p1 = reinterpret_cast<const uint32_t *>(colL + c2.w);
-                        const u32x2 v0 = u32x2{p0[0], p0[1]};
-                        const u32x2 v1 = u32x2{p1[0], p1[1]};
-                        acc0 = pk_mad(__builtin_amdgcn_perm(v0.y, v0.x, s01[m]), c2.x, acc0);
-                        acc1 = pk_mad(__builtin_amdgcn_perm(v0.y, v0.x, s23[m]), c2.x, acc1);
-                        acc0 = pk_mad(__builtin_amdgcn_perm(v1.y, v1.x, s01[m]), c2.z, acc0);
-                        acc1 = pk_mad(__builtin_amdgcn_perm(v1.y, v1.x, s23[m]), c2.z, acc1);
-                    }
-                    if (LZ && deno != 0) {  // masked + renormalised border row: int16(nume * 64 / deno)
-                        auto dv = [&](uint32_t pr) {
-                            const int lo = exact_div(static_cast<int>(static_cast<int16_t>(pr & 0xffffu)) * 64, deno);
-                            const int hi = exact_div(static_cast<int>(static_cast<int16_t>(pr >> 16)) * 64, deno);
-                            return (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16);
-                        };
-                        acc0 = dv(acc0);
-                        acc1 = dv(acc1);
-                    }
-                    *reinterpret_cast<u32x2 *>(wout + 2 * u) = u32x2{acc0, acc1};
-                }
-            }
+            for (int k = 0; k < 4; ++k)
+                bytes[k] = static_cast<uint32_t>(min(max(v[k], 0), 255));
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bytes[k] = min((static_cast<uint32_t>(sum[k]) >> 23) & 0xffffu, 255u);
         }
-    }
-    wait_vmcnt<0>();  // no LDS-DMA may still be writing when the workgroup's LDS is released
+        const uint32_t o = opaque(bytes[0] | (bytes[1] << 8)) | (bytes[2] << 16) | (bytes[3] << 24);
+        if (!EDGE) {
+            __builtin_amdgcn_raw_buffer_store_b32(o, dstR, off, 0, 0);
+            return;
+        }
+        const bool whole = hq && dstA4 && x0 + 4 <= t.dstW;
+        __builtin_amdgcn_raw_buffer_store_b32(o, dstR, whole ? off : OOB, 0, 0);
+        if (hq && !whole) {  // frame edge / unaligned destination: bytes
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (x0 + k < t.dstW)
+                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(bytes[k]), dstR, off + k, 0, 0);
+        }
+    };
+
+    // D register sets, one per row mod D: the loop body is straight-line, so the compiler's vmcnt
+    // waits count the loads in flight exactly (the tables are padded past the end)
+    auto walk = [&](auto edge) {
+        uint32_t b[D][NV][NV];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            issue(sload(W.segs + 2 * (y0 + d)).x, b[d]);
+        int4 g = sload(W.segs + 2 * y0);
+        int s = y0;
+        for (; s + D <= y1; s += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                segment(edge, s + d, g, b[d]);
+        }
+#pragma unroll
+        for (int d = 0; d < D - 1; ++d)
+            if (s + d < y1)
+                segment(edge, s + d, g, b[d]);
+    };
+    if (interior)
+        walk(std::integral_constant<bool, false>());
+    else
+        walk(std::integral_constant<bool, true>());
 }
 
 // ================================================================ Area integer ratio
@@ -2149,12 +2174,6 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
     return hipLaunchKernel(kern, grid, dim3(256), args, lds, s);
 }
 
-size_t walk_lds_bytes(const WalkDev &w, int rowsPerBand)
-{
-    return static_cast<size_t>(w.R) * w.pitch + 2 * 8 * static_cast<size_t>(w.maxUnits) +
-           static_cast<size_t>(rowsPerBand) * (8 * w.t.nYp + 16) + 256;
-}
-
 hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
@@ -2168,13 +2187,31 @@ hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd,
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24))
         return hipErrorInvalidValue;
     const void *kern = nullptr;
+    // (NP, VY = 2NP or 2NP - 2, NV) instantiations
+    const int e = 2 * t.NP - t.nYp;
+    if ((e != 0 && e != 2) || t.nYp < 2 || (w.NV != 1 && w.NV != 2))
+        return hipErrorInvalidValue;
+#define IQO_WALK_NV(NP_, VY_, NV_)                                                                   \
+    kern = t.lanczos ? reinterpret_cast<const void *>(walk_kernel<NP_, VY_, NV_, true>)              \
+                     : reinterpret_cast<const void *>(walk_kernel<NP_, VY_, NV_, false>);
+#define IQO_WALK_VY(NP_, VY_)                                                                        \
+    if (w.NV == 1) {                                                                                 \
+        IQO_WALK_NV(NP_, VY_, 1)                                                                     \
+    } else {                                                                                         \
+        IQO_WALK_NV(NP_, VY_, 2)                                                                     \
+    }
 #define IQO_WALK(NP_)                                                                                \
     case NP_:                                                                                        \
-        kern = t.lanczos ? reinterpret_cast<const void *>(walk_kernel<NP_, true>)                    \
-                         : reinterpret_cast<const void *>(walk_kernel<NP_, false>);                  \
+        if (e == 0) {                                                                                \
+            IQO_WALK_VY(NP_, 2 * NP_)                                                                \
+        } else {                                                                                     \
+            IQO_WALK_VY(NP_, 2 * NP_ - 2)                                                            \
+        }                                                                                            \
         break;
     switch (t.NP) {
-        IQO_WALK(1)
+    case 1:
+        IQO_WALK_VY(1, 2)
+        break;
         IQO_WALK(2)
         IQO_WALK(3)
         IQO_WALK(4)
@@ -2186,24 +2223,26 @@ hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd,
         return hipErrorInvalidValue;
     }
 #undef IQO_WALK
-    // bands per frame: fill whole rounds of resident workgroups, each band at most maxBand rows
-    // (its tap records live in LDS) and long enough to amortise the window fill
+#undef IQO_WALK_VY
+#undef IQO_WALK_NV
+    const int lds = 4 * w.waveBytes;
+    // bands per frame: about 2.5 rounds of resident waves (more waves than slots hide the tail and
+    // the latency of each wave's serial walk; MI355X G1/G2/G3 sweeps), bands of >= 16 rows
     if (bands <= 0) {
-        const int rpbMax = std::min(rows, w.maxBand);
-        const int resident = resident_waves(kern, 256, static_cast<int>(walk_lds_bytes(w, rpbMax))) / 4;
-        bands = choose_bands(rows, io.frames * w.nTx, 1, std::max(1, resident), t.nYp);
+        const int64_t resident = std::max(1, resident_waves(kern, 256, lds));
+        const int64_t perBand = static_cast<int64_t>(w.nS) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
     }
-    bands = std::max(bands, (rows + w.maxBand - 1) / w.maxBand);
     bands = std::max(1, std::min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
-    const uint64_t nWG = static_cast<uint64_t>(w.nTx) * static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames);
-    if (nWG >= (uint64_t(1) << 31))
+    const uint64_t nWaves = static_cast<uint64_t>(w.nS) * static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     WalkArgs a{w, io, rowBegin, rowEnd, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
-               static_cast<unsigned>(nWG), w.maxNew * w.cpw};
+               static_cast<unsigned>(nWaves)};
     void *args[] = {&a};
-    return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nWG)), dim3(256), args, walk_lds_bytes(w, rpb), s);
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, lds, s);
 }
 
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)

@@ -46,19 +46,21 @@ struct TileDev {
 };
 hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
 
-// --- general-ratio band walker: the tile tables walked band by band, each source row fetched
-// once per band into an LDS ring (LDS-DMA, dword lanes; 4-byte aligned source layouts).
+// --- general-ratio wave walker: every wave walks a 256-column strip of one band of rows through
+// a private LDS ring of source rows widened to u16 (plan.hpp WalkTables; 4-byte aligned sources).
 struct WalkDev {
-    TileDev t;                   // tables (t.spans / CT / TH unused)
-    int CTW, nTx;                // output columns per column tile, column tiles
-    const int2 *wspans;          // {lo8, units} per column tile; a unit = 4 work columns
-    int maxUnits;                // units of the widest tile
-    int R, pitch;                // ring rows (power of 2), ring row pitch (bytes, multiple of 256)
-    int chunks, cpw, maxNew;     // 256-B DMA chunks per ring row, chunks per wave, new rows per output row
-    int maxBand;                 // rows per band at most (tap records of a band live in LDS)
+    TileDev t;                   // column tables (cols, colCoef, colA, nQp), lanczos, srcW / dstW, NP
+    int nS;                      // 256-output strips per row
+    const int4 *spans;           // {lo8, units, interior, 0} per strip; a unit = 4 work columns
+    int NV;                      // units per lane (1, 2)
+    int R, pitch;                // ring rows, ring row pitch (bytes)
+    int waveBytes;               // LDS per wave: ring + work row + sink
+    const uint32_t *rowTap;      // (dstH + 1) x VY x {(c, c) splat, ring byte offset of the clamped row}
+    const int4 *rows;            // {lo, hi, hi % R, deno} per output row
+    const int4 *segs;            // 2 per row: {first, ring offset of first, border, first of row
+                                 // + kWalkD}, {yM, yS, yNeg, 0} (plan.hpp WalkSeg; padded past the end)
 };
 hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
-size_t walk_lds_bytes(const WalkDev &w, int rowsPerBand);
 
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {

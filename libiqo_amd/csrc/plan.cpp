@@ -856,71 +856,93 @@ void band_src_rows(const Plan &p, int r0, int r1, int *s0, int *s1)
     *s1 = hi;
 }
 
-// The walker's tables: the tile tables' rows and columns, its own column tiling and ring.
+// The wave walker's tables: the tile tables' rows and column coefficients, 256-column strips, the
+// ring geometry and per-row tap records that carry ring byte offsets (the ring slot of source row
+// r is r % R for every band, so the offsets are constants of the plan).
 void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w)
 {
     *w = WalkTables();
-    if (!t.ok || t.nYp > 64 || p.srcW < 4 || t.NP > 8)
+    // the vertical taps are unrolled as 2 * NP or 2 * NP - 2 (the same ratio on both axes: the
+    // horizontal pairs also absorb an odd window start), NP <= 8
+    if (!t.ok || p.srcW < 4 || t.NP > 8 || t.nYp < 2 || (t.nYp != 2 * t.NP && t.nYp != 2 * t.NP - 2))
         return;
-    // column tiles: as few as keep a tile within 1024 output columns (one quad per thread) and
-    // 2048 work columns (two 4-column units per thread)
-    int nT = (p.dstW + 1023) / 1024;
-    for (;; ++nT) {
-        const int ctw = ((p.dstW + nT - 1) / nT + 3) & ~3;
-        int maxU = 0;
-        std::vector<WalkSpan> sp(static_cast<size_t>(nT));
-        bool ok = true;
-        for (int k = 0; k < nT && ok; ++k) {
-            const int x0 = k * ctw, x1 = std::min(p.dstW, x0 + ctw);
-            if (x0 >= x1) {
-                ok = false;
-                break;
-            }
-            int lo = 1 << 30, hi = -(1 << 30);
-            for (int x = x0; x < x1; ++x) {
-                lo = std::min(lo, t.cols[static_cast<size_t>(x)].a);
-                hi = std::max(hi, t.cols[static_cast<size_t>(x)].a + 2 * t.NP);
-            }
-            const int lo8 = lo & ~7;
-            const int units = (hi - lo8 + 3) / 4;
-            sp[static_cast<size_t>(k)] = WalkSpan{lo8, units};
-            maxU = std::max(maxU, units);
+    const int nS = (p.dstW + kWalkStrip - 1) / kWalkStrip;
+    int maxU = 1;
+    w->spans.resize(static_cast<size_t>(nS));
+    for (int k = 0; k < nS; ++k) {
+        const int x0 = k * kWalkStrip, x1 = std::min(p.dstW, x0 + kWalkStrip);
+        int lo = 1 << 30, hi = -(1 << 30);
+        for (int x = x0; x < x1; ++x) {
+            lo = std::min(lo, t.cols[static_cast<size_t>(x)].a);
+            hi = std::max(hi, t.cols[static_cast<size_t>(x)].a + 2 * t.NP);
         }
-        if (!ok || nT > 64)
-            return;
-        if (maxU > 512)
-            continue;
-        w->CTW = ctw;
-        w->nTx = nT;
-        w->spans = sp;
-        w->maxUnits = maxU;
-        break;
+        const int lo8 = lo & ~7;
+        const int units = (hi - lo8 + 3) / 4;
+        bool interior = x1 - x0 == kWalkStrip;
+        for (int x = x0; x < x1; ++x)
+            interior = interior && t.cols[static_cast<size_t>(x)].D == 0;
+        w->spans[static_cast<size_t>(k)] = WalkSpan{lo8, units, interior ? 1 : 0};
+        maxU = std::max(maxU, units);
     }
-    // ring: rows spanned by any output row and the kWalkPrefetch rows after it
-    int need = 1, maxNew = 1;
+    const int NV = maxU <= 64 ? 1 : (maxU <= 128 ? 2 : 0);
+    if (!NV)
+        return;  // a strip reads more than 512 source columns (downscales beyond ~1.9x)
+    int win = 1, maxNew = 0;
     for (int y = 0; y < p.dstH; ++y) {
-        const int y2 = std::min(y + kWalkPrefetch, p.dstH - 1);
-        need = std::max(need, t.rows[static_cast<size_t>(y2)].hi - t.rows[static_cast<size_t>(y)].lo + 1);
+        const TileRec &r = t.rows[static_cast<size_t>(y)];
+        win = std::max(win, r.hi - r.lo + 1);
         if (y > 0)
-            maxNew = std::max(maxNew, t.rows[static_cast<size_t>(y)].hi - t.rows[static_cast<size_t>(y - 1)].hi);
+            maxNew = std::max(maxNew, r.hi - t.rows[static_cast<size_t>(y - 1)].hi);
     }
-    int R = 1;
-    while (R < need)
-        R *= 2;
+    if (maxNew > NV)
+        return;  // the load pipeline carries NV rows per output row
+    // rows first(y) .. first(y)+NV-1 are widened at row y, up to NV-1 of them early: R = the widest
+    // window + NV keeps every slot they overwrite dead
+    const int R = win + NV;
+    w->NV = NV;
+    w->nS = nS;
+    w->maxUnits = maxU;
     w->R = R;
-    w->pitch = (4 * w->maxUnits + 8 + 255) & ~255;
-    w->chunks = w->pitch / 256;
-    w->cpw = (w->chunks + 3) / 4;
+    w->pitch = NV == 1 ? 512 : 8 * maxU;
     w->maxNew = maxNew;
-    // DMAs per wave per output row stay small enough for the constant waits (kernels.hip)
-    if (maxNew * w->cpw > 8)
+    w->waveBytes = static_cast<size_t>(R) * w->pitch + 512u * NV + (NV == 2 ? 512u : 0u);
+    if (4 * w->waveBytes > 64 * 1024)
         return;
-    // bands: tap records (8 B per tap) and row records (16 B) of a band in at most 24 KiB
-    w->maxBand = std::max(1, std::min(512, 24 * 1024 / (8 * t.nYp + 16)));
-    const size_t lds = static_cast<size_t>(R) * w->pitch + 2 * 8 * static_cast<size_t>(w->maxUnits) +
-                       static_cast<size_t>(w->maxBand) * (8 * t.nYp + 16) + 256;
-    if (lds > 64 * 1024)
-        return;
+    const int H = p.dstH;
+    w->rows.resize(static_cast<size_t>(H));
+    std::vector<int> first(static_cast<size_t>(H));
+    for (int y = 0; y < H; ++y)
+        first[static_cast<size_t>(y)] = y ? t.rows[static_cast<size_t>(y - 1)].hi + 1 : t.rows[0].lo;
+    w->segs.resize(static_cast<size_t>(H) + kWalkPrefetch + 1);
+    for (int y = 0; y < H + kWalkPrefetch + 1; ++y) {
+        const int yy = std::min(y, H - 1);
+        const TileRec &r = t.rows[static_cast<size_t>(yy)];
+        const int f = first[static_cast<size_t>(yy)];
+        const int fD = first[static_cast<size_t>(std::min(y + kWalkPrefetch, H - 1))];
+        WalkSeg g{f, (f % R) * w->pitch, r.deno != 0, fD, 0u, 0, 0, 0};
+        if (r.deno != 0 && r.deno != 0x7fffffff) {  // 0x7fffffff: masked divisor 0, quotient 0
+            const int32_t ad = r.deno < 0 ? -r.deno : r.deno;
+            if (!magic_y(ad, &g.yM, &g.yS))
+                return;  // outside the proven range of the multiply-high division: tile_kernel
+            g.yNeg = r.deno < 0;
+        }
+        w->segs[static_cast<size_t>(y)] = g;
+    }
+    if (static_cast<size_t>(R) * w->pitch > 65535)
+        return;  // ring offsets are 16-bit
+    w->rowTap.resize(static_cast<size_t>(H + 1) * t.nYp * 2);
+    for (int y = 0; y < H + 1; ++y) {
+        const int yy = std::min(y, H - 1);
+        const TileRec &r = t.rows[static_cast<size_t>(yy)];
+        if (y < H)
+            w->rows[static_cast<size_t>(y)] = WalkRow{r.lo, r.hi, r.hi % R, r.deno};
+        for (int i = 0; i < t.nYp; ++i) {
+            const int row = std::min(std::max(r.start + i, r.lo), r.hi);
+            const size_t k = (static_cast<size_t>(y) * t.nYp + i) * 2;
+            w->rowTap[k] = t.rowCoef[static_cast<size_t>(yy) * t.nYp + i];
+            w->rowTap[k + 1] = static_cast<uint32_t>((row % R) * w->pitch);
+        }
+    }
     w->ok = true;
 }
 

@@ -152,18 +152,39 @@ bool tile_set_rows(const Plan &p, TileTables *t, int TH);
 // its work-column span in 4-column units, and an LDS ring of R source rows.
 struct WalkSpan {
     int32_t lo8, units;           // first work column (multiple of 8), 4-column units
+    int32_t interior;             // 256 columns, none of them a masked border column
 };
+struct WalkRow {
+    int32_t lo, hi;               // clamped source row window of the output row
+    int32_t hiSlot;               // hi % R
+    int32_t deno;                 // masked border row divisor (0: none)
+};
+struct WalkSeg {
+    int32_t first;                // first source row the output row needs that its predecessor did not
+    int32_t slotOff;              // ring byte offset of that row ((first % R) * pitch)
+    int32_t border;               // masked border row: int16(n * 64 / deno) by magic_y (yM, yS)
+    int32_t firstD;               // first of the output row kWalkPrefetch below (the load look-ahead)
+    uint32_t yM;                  // 0 for a divisor of 0 (quotient 0, as in general_kernel)
+    int32_t yS, yNeg, pad;        // yNeg: the divisor is negative
+};
+// The wave walker (kernels.hip walk_kernel): every wave owns a strip of kWalkStrip output columns
+// of one band of rows and walks it top to bottom through a private LDS ring of R source rows,
+// widened to u16 (8 bytes per 4-column unit, NV units per lane).
+constexpr int kWalkStrip = 256;   // output columns per wave (4 per lane, one dword store)
+constexpr int kWalkPrefetch = 4;  // output rows of load look-ahead (kernels.hip kWalkD)
 struct WalkTables {
     bool ok = false;
-    int CTW = 0, nTx = 0;
-    std::vector<WalkSpan> spans;  // nTx
-    int maxUnits = 0;             // at most 512 (two units per thread)
-    int R = 0, pitch = 0;         // ring rows (power of 2), ring row pitch (multiple of 256)
-    int chunks = 0, cpw = 0;      // 256-B DMA chunks per row, per wave (4 waves)
-    int maxNew = 0;               // most source rows first needed by one output row
-    int maxBand = 0;              // rows per band at most (tap records of a band in LDS)
+    int NV = 0;                   // units per lane (1, 2): a strip reads at most 256 * NV source columns
+    int nS = 0;                   // strips per row
+    std::vector<WalkSpan> spans;  // nS
+    int maxUnits = 0;             // <= 64 * NV
+    int R = 0, pitch = 0;         // ring rows (widest row window + NV), ring row pitch (bytes)
+    int maxNew = 0;               // most source rows first needed by one output row (<= NV)
+    std::vector<WalkRow> rows;    // dstH
+    std::vector<WalkSeg> segs;    // dstH + kWalkPrefetch + 1 (the look-ahead reads past the last row)
+    std::vector<uint32_t> rowTap; // (dstH + 1) x nYp x {coef splat, ring byte offset of the clamped row}
+    size_t waveBytes = 0;         // LDS per wave: ring + work row + sink
 };
-constexpr int kWalkPrefetch = 3;  // output rows of DMA look-ahead (kernels.hip kWalkD)
 void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w);
 
 // Build the full plan.  Returns false (with *err) for invalid arguments.

@@ -39,19 +39,19 @@ def test_native_library_is_the_gpu_path():
     assert r.describe()["kernel"] == "lanczos_stream"
 
 
-@pytest.mark.parametrize("force_general", [False, True])
-def test_golden_vectors_gpu(golden, force_general):
+@pytest.mark.parametrize("variant", ["default", "walk", "force_general"])
+def test_golden_vectors_gpu(golden, variant):
     """Every golden case, via the host-pointer entry point (reference resize() semantics): default
-    kernels (the separable tile kernel for every shape without a specialised one) and the
-    one-row-per-workgroup general_kernel."""
+    kernels (the separable tile kernel for every shape without a specialised one), the band
+    walker (plan option walk = 1) and the one-row-per-workgroup general_kernel."""
     n = 0
     for c in golden["cases"]:
         sw, sh, dw, dh = c["srcW"], c["srcH"], c["dstW"], c["dstH"]
         if sw * sh > 4_000_000:
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
-        if force_general:
-            r.set_option("force_general", 1)
+        if variant != "default":
+            r.set_option(variant, 1)
         src = ol.gen(c["gen"], sw, sh, c["seed"])
         out = _run_host(r, src, dw, dh)
         exp = _expected(c)
