@@ -50,9 +50,9 @@ struct iqo_hip_plan {
     uint32_t *dTColCoef = nullptr;
     int32_t *dTColA = nullptr;
     int tileNQp = 0;
-    // general-ratio band walker over the same tables (option "walk" = 0 keeps tile_kernel)
+    // general-ratio wave walker (plan.hpp WalkTables; option "walk" = 0 keeps tile_kernel)
     iqo_amd::WalkTables wt;
-    bool useWalk = false;
+    bool useWalk = true;
     int4 *dWSpans = nullptr;
     int4 *dWSegs = nullptr;
     uint32_t *dWRowTap = nullptr;
@@ -791,7 +791,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->useTile = value != 0;
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "walk")) {  // 0: general ratios use tile_kernel instead of the band walker
+    if (!std::strcmp(key, "walk")) {  // 0: general ratios use tile_kernel instead of the wave walker
         h->useWalk = value != 0;
         return IQO_HIP_OK;
     }

@@ -100,10 +100,11 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 2, 640, 480, 320, 240, 1), "lanczos_stream"),
     (("area", 0, 7680, 4320, 1920, 1080, 1), "area_int"),
     (("linear", 0, 1920, 1080, 3840, 2160, 1), "linear_up2"),
-    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "tile"),          # general ratios: tile kernel (walk=1 opts into the band walker)
-    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "tile"),
-    (("area", 0, 1920, 1080, 1280, 720, 1), "tile"),
-    (("linear", 0, 1366, 768, 1000, 1000, 1), "tile"),
+    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "walk"),          # general ratios: wave walker
+    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "walk"),
+    (("area", 0, 1920, 1080, 1280, 720, 1), "walk"),
+    (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),
+    (("lanczos", 3, 13, 9, 5, 40, 1), "tile"),                    # 13 columns: no 256-column strip fits the walker's tables
     (("lanczos", 9, 64, 48, 1000, 900, 1), "tile"),               # 64 work columns per row window: tiles
     (("lanczos", 3, 1920, 1080, 960, 540, 2), "lanczos_stream"),   # pxScale-2 chroma (ring streamer)
     (("lanczos", 9, 4000, 3000, 97, 61, 1), "general"),           # 2 x 9 x 41 taps: beyond NP = 16

@@ -39,18 +39,20 @@ def test_native_library_is_the_gpu_path():
     assert r.describe()["kernel"] == "lanczos_stream"
 
 
-@pytest.mark.parametrize("variant", ["default", "walk", "force_general"])
+@pytest.mark.parametrize("variant", ["default", "tile", "force_general"])
 def test_golden_vectors_gpu(golden, variant):
     """Every golden case, via the host-pointer entry point (reference resize() semantics): default
-    kernels (the separable tile kernel for every shape without a specialised one), the band
-    walker (plan option walk = 1) and the one-row-per-workgroup general_kernel."""
+    kernels (the wave walker for shapes without a specialised kernel, where its tables fit), the
+    separable tile kernel (plan option walk = 0) and the one-row-per-workgroup general_kernel."""
     n = 0
     for c in golden["cases"]:
         sw, sh, dw, dh = c["srcW"], c["srcH"], c["dstW"], c["dstH"]
         if sw * sh > 4_000_000:
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
-        if variant != "default":
+        if variant == "tile":
+            r.set_option("walk", 0)
+        elif variant != "default":
             r.set_option(variant, 1)
         src = ol.gen(c["gen"], sw, sh, c["seed"])
         out = _run_host(r, src, dw, dh)
@@ -370,18 +372,19 @@ TILE_SHAPES = [
 
 @pytest.mark.parametrize("cfg", TILE_SHAPES, ids=lambda c: "%s%d_%dx%d_%dx%d" % c[:6])
 def test_tile_streamer_matches_oracle(cfg):
-    """General ratios (shapes without a specialised kernel): the separable tile kernel (the
-    default; every misaligned layout: 8-byte, 12-byte-shifted and single-byte loads; dword and
-    byte stores), the band walker (plan option walk = 1 on 4-byte aligned sources; several band
-    splits and a padded stride) equal the oracle, and general_kernel (tile = 0) on the same batch."""
+    """General ratios (shapes without a specialised kernel): the wave walker (the default on
+    4-byte aligned sources where its tables fit; several band splits and a padded stride), the
+    separable tile kernel (plan option walk = 0, and every misaligned layout: 8-byte,
+    12-byte-shifted and single-byte loads; dword and byte stores) equal the oracle, and
+    general_kernel (tile = 0) on the same batch."""
     m, d, sw, sh, dw, dh, px = cfg
     frames = _noise_batch(2, sw, sh, 1100)
     frames[1, :, : sw // 3] = 255
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
     t = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    t.set_option("walk", 0)
     assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    r.set_option("walk", 1)
     kern = r.describe()["kernel"]
     assert kern in ("walk", "tile")
     src = torch.from_numpy(frames).to(DEV)
@@ -393,7 +396,6 @@ def test_tile_streamer_matches_oracle(cfg):
     if kern == "walk":
         for bands in (1, 3, 7, dh):
             w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-            w.set_option("walk", 1)
             w.set_option("bands", bands)
             out = w.resize_tensor(src).cpu().numpy()
             for f in range(2):
