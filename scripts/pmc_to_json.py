@@ -18,9 +18,10 @@ import statistics
 import sys
 
 KERNELS = {"lanczos_stream": "lanczos_s", "area_int": "area_int_kernel",  # lanczos_s: symb / sym / stream
-           "linear_up2": "linear_up2_kernel", "general": "general_kernel", "tile": "tile_kernel"}
-BENCH = {"c2": ("lanczos_stream", 128), "c3": ("area_int", 48), "c4": ("linear_up2", 128), "c1": ("lanczos_stream", 4096),
-         "g1": ("tile", 128), "g2": ("tile", 32), "g3": ("tile", 128)}
+           "linear_up2": "linear_up2_kernel", "general": "general_kernel", "tile": "tile_kernel",
+           "walk": "walk_kernel"}
+BENCH = {"c2": ("lanczos_stream", 128), "c3": ("area_int", 64), "c4": ("linear_up2", 256), "c1": ("lanczos_stream", 4096),
+         "g1": ("walk", 128), "g2": ("walk", 32), "g3": ("walk", 128)}
 
 
 def per_dispatch(dirname, counter, kname):
