@@ -53,6 +53,9 @@ struct iqo_hip_plan {
     // general-ratio wave walker (plan.hpp WalkTables; option "walk" = 0 keeps tile_kernel)
     iqo_amd::WalkTables wt;
     bool useWalk = true;
+    // exact 2x Lanczos upscale kernel on the main rows x middle columns (option "up2" = 0: walker only)
+    iqo_amd::Up2Tables ut;
+    bool useUp2 = true;
     int4 *dWSpans = nullptr;
     int4 *dWSegs = nullptr;
     uint32_t *dWRowTap = nullptr;
@@ -362,6 +365,7 @@ int upload_tile(iqo_hip_plan *h)
             rc = upload(&h->dWSegs, sg.data(), sg.size());
         if (rc)
             return rc;
+        iqo_amd::build_up2(h->p, h->wt, &h->ut);
     }
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
@@ -558,6 +562,24 @@ iqo_amd::WalkDev walk_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::Up2Dev up2_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::Up2Tables &u = h->ut;
+    iqo_amd::Up2Dev d;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.NT = u.NT;
+    d.colLo = u.colLo;
+    d.colHi = u.colHi;
+    d.cy0 = u.cy0;
+    d.cx0 = u.cx0;
+    std::memcpy(d.cy1, u.cy1, sizeof d.cy1);
+    std::memcpy(d.cx1, u.cx1, sizeof d.cx1);
+    return d;
+}
+
 iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
 {
     const Plan &p = h->p;
@@ -596,6 +618,10 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     // the wave walker loads aligned dwords: 4-byte aligned source frames and rows
     if (kernel == IQO_KERNEL_TILE && h->wt.ok && h->useWalk && aligned(src, 4, srcSt, srcFrameSt))
         kernel = IQO_KERNEL_WALK;
+    // the 2x Lanczos kernel loads 8 B per lane and stores 16 B per lane
+    if (kernel == IQO_KERNEL_WALK && h->ut.ok && h->useUp2 && aligned(src, 8, srcSt, srcFrameSt) &&
+        aligned(dst, 16, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_LANCZOS_UP2;
     return kernel;
 }
 
@@ -663,6 +689,21 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_tile(tile_dev(h), io, rb, re, s);
         else if (kernel == IQO_KERNEL_WALK)
             e = iqo_amd::launch_walk(walk_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_LANCZOS_UP2) {
+            // the walker takes the two edge strips (all rows) and the border rows of the middle
+            // strips; lanczos_up2_kernel the main rows of the middle strips
+            const iqo_amd::WalkDev wd = walk_dev(h);
+            const iqo_amd::Up2Tables &u = h->ut;
+            const int nS = h->wt.nS;
+            const int f0 = std::max(rb, u.m0), f1 = std::min(re, u.m1);
+            e = iqo_amd::launch_walk(wd, io, rb, re, h->bands, s, 0, 2, nS - 1);
+            if (e == hipSuccess && rb < std::min(re, u.m0))
+                e = iqo_amd::launch_walk(wd, io, rb, std::min(re, u.m0), h->bands, s, 1, nS - 2, 1);
+            if (e == hipSuccess && f0 < f1)
+                e = iqo_amd::launch_up2(up2_dev(h), io, f0, f1, h->bands, s);
+            if (e == hipSuccess && std::max(rb, u.m1) < re)
+                e = iqo_amd::launch_walk(wd, io, std::max(rb, u.m1), re, h->bands, s, 1, nS - 2, 1);
+        }
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -726,7 +767,8 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->phasesY = h->p.y.phases;
     d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL
                                 : (h->p.kernel == IQO_KERNEL_GENERAL && h->tt.ok && h->useTile
-                                       ? (h->wt.ok && h->useWalk ? IQO_KERNEL_WALK : IQO_KERNEL_TILE)
+                                       ? (h->wt.ok && h->useWalk ? (h->ut.ok && h->useUp2 ? IQO_KERNEL_LANCZOS_UP2 : IQO_KERNEL_WALK)
+                                                                 : IQO_KERNEL_TILE)
                                        : h->p.kernel);
     d->bandsPerFrame = h->bands;
     return IQO_HIP_OK;
@@ -789,6 +831,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "tile")) {  // 0: shapes without a specialised kernel use general_kernel
         h->useTile = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "up2")) {  // 0: exact 2x Lanczos upscales use the wave walker alone
+        h->useUp2 = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "walk")) {  // 0: general ratios use tile_kernel instead of the wave walker
@@ -1296,7 +1342,10 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     if (!h.tt.ok)
         return IQO_KERNEL_GENERAL;
     iqo_amd::build_walk_tables(h.p, h.tt, &h.wt);
-    return h.wt.ok && h.useWalk ? IQO_KERNEL_WALK : IQO_KERNEL_TILE;
+    if (!h.wt.ok || !h.useWalk)
+        return IQO_KERNEL_TILE;
+    iqo_amd::build_up2(h.p, h.wt, &h.ut);
+    return h.ut.ok && h.useUp2 ? IQO_KERNEL_LANCZOS_UP2 : IQO_KERNEL_WALK;
 }
 
 } // extern "C"

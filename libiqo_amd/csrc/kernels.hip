@@ -1440,7 +1440,8 @@ struct WalkArgs {
     Io io;
     int rowBegin, rowEnd, rowsPerBand, bands;
     int srcBytes, dstBytes;
-    unsigned nWaves;  // nS * bands * frames
+    unsigned nWaves;  // strips * bands * frames
+    int stripLo, strips, stripStride;  // the strips walked: stripLo + i * stripStride, i < strips
 };
 
 constexpr int kWalkD = 4;  // load look-ahead in output rows (plan.hpp kWalkPrefetch)
@@ -1473,8 +1474,8 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a)
     const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;  // whole wave; the kernel has no barrier
-    const int strip = static_cast<int>(gw % static_cast<unsigned>(W.nS));
-    const unsigned rest = gw / static_cast<unsigned>(W.nS);
+    const int strip = a.stripLo + static_cast<int>(gw % static_cast<unsigned>(a.strips)) * a.stripStride;
+    const unsigned rest = gw / static_cast<unsigned>(a.strips);
     const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
     const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
     const int y0 = a.rowBegin + band * a.rowsPerBand;
@@ -1980,6 +1981,165 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 }
 
 
+// ================================================================ exact 2x Lanczos upscale
+//
+// Lanczos-2/3 at exactly 2x (pxScale 1), main rows x middle columns (plan.cpp build_up2; the wave
+// walker does the edge strips and the border rows).  In the reference's tables for this ratio an
+// even output row / column sits exactly on a source sample (a single tap: 64 vertically, 2^14
+// horizontally) and an odd one takes NT = 2 * degree taps starting NT/2 - 1 samples to its left
+// (IQOLanczosResizerImpl_Generic.cpp:144-190, 404-454).  The linear_up2 streamer's layout: one
+// WAVE per (row band, 992-column output strip, frame) walks the band's SOURCE rows top to bottom;
+// lane l owns source columns [cb, cb + 8) and (lanes 1..62) output columns [2cb, 2cb + 16).
+//
+// Every source row is loaded once per band (8 B per lane, NT rows ahead) and widened to four u16
+// pairs in a register window of NT rows (static names: the loop is unrolled NT times).  Source
+// step k yields output rows 2k (one packed multiply per pair) and 2k+1 (NT packed MACs), the
+// coefficient splats in SGPRs.  The horizontal pass needs work columns [cb - 3, cb + 11): the two
+// pairs either side come from the neighbouring lanes by DPP, odd-aligned pairs by v_alignbit;
+// output 2cb + j is one (j even) or NT/2 (j odd) v_dot2_i32_i16 on pairs chosen at compile time.
+// Sixteen outputs pack into one 16-B store per lane.  Arithmetic as everywhere: int16-wrapping
+// vertical pass, (s + 2^19) >> 20 saturated to u8.
+
+struct Up2Args {
+    Up2Dev u;
+    Io io;
+    int rowBegin, rowEnd, rowsPerBand, bands, wavesPerRow;
+    int srcBytes, dstBytes;
+    unsigned nWaves;
+};
+
+template <int NT>
+__global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
+{
+    constexpr int NW = NT;           // register window rows
+    constexpr int H = NT / 2;        // coefficient pairs of an odd output
+    constexpr int OFF = 1 - NT / 2;  // window start relative to x >> 1 (y >> 1)
+    constexpr int OOB = 0x7ff00000;
+    const Up2Dev &u = a.u;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;  // whole wave; no barrier in this kernel
+    const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
+    const unsigned rest = gw / static_cast<unsigned>(a.wavesPerRow);
+    const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+
+    const int xs0 = u.colLo / 2 + wcol * 62 * 8;  // first source column of lane 1
+    const int cb = xs0 - 8 + 8 * lane;
+    const bool produce = lane >= 1 && lane <= 62 && 2 * cb < u.colHi;
+    const int voff = cb + 8 <= u.srcW ? cb : OOB;  // the middle columns never need cb < 0
+    const int stoff = produce ? 2 * cb : OOB;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+
+    // source steps k: output rows 2k, 2k+1 (those outside [y0, y1) are computed and dropped);
+    // step k reads source rows k + OFF .. k + OFF + NT - 1
+    const int kLo = y0 >> 1, kHi = (y1 + 1) >> 1;
+    const int rFirst = kLo + OFF;
+    const int rLast = kHi - 1 + OFF + NT - 1;
+    // rows of dropped outputs may lie outside the window: clamped (their values are never used)
+    const int srcLast = a.io.srcRowEnd - 1;
+    auto load_row = [&](int r) -> u32x2 {
+        const int rc = min(max(r, srcRow0), srcLast);
+        return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff, r <= rLast ? (rc - srcRow0) * srcSt : OOB, 0);
+    };
+    auto widen = [&](u32x2 v, uint32_t (&P)[4]) {
+        P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
+        P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
+        P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
+        P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);  // (cb+6, cb+7)
+    };
+    // horizontal pass + store of output row y from the lane's four work pairs
+    auto emit = [&](const uint32_t (&Wk)[4], int y, bool valid) {
+        uint32_t E[8];  // E[e] = work columns (cb - 4 + 2e, cb - 3 + 2e)
+        E[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(Wk[2]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+        E[1] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(Wk[3]), 0x138, 0xf, 0xf, true));
+        E[2] = Wk[0];
+        E[3] = Wk[1];
+        E[4] = Wk[2];
+        E[5] = Wk[3];
+        E[6] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(Wk[0]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        E[7] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(Wk[1]), 0x130, 0xf, 0xf, true));
+        uint32_t O[7];  // O[e] = work columns (cb - 3 + 2e, cb - 2 + 2e)
+#pragma unroll
+        for (int e = 0; e < 7; ++e)
+            O[e] = __builtin_amdgcn_alignbit(E[e + 1], E[e], 16);
+        auto pair = [&](int rel) { return (rel & 1) ? O[(rel - 1) / 2] : E[rel / 2]; };  // low half = column rel
+        int sum[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if ((j & 1) == 0) {
+                // on a source column: c * w[cb + j/2] (the pair's high half meets a zero coefficient)
+                sum[j] = sdot2(pair((j >> 1) + 4), u.cx0, 1 << 19);
+            } else {
+                const int rel = (j >> 1) + OFF + 4;
+                int acc = 1 << 19;
+#pragma unroll
+                for (int q = 0; q < H; ++q)
+                    acc = sdot2(pair(rel + 2 * q), u.cx1[q], acc);
+                sum[j] = acc;
+            }
+        }
+        u32x4 o;
+        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+        o.z = pack_hi(pack_lo(sum[8], sum[9]), sum[10], sum[11]);
+        o.w = pack_hi(pack_lo(sum[12], sum[13]), sum[14], sum[15]);
+        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, stoff, valid ? (y - dstRow0) * dstSt : OOB, 0);
+    };
+
+    uint32_t R[NW][4];
+    // the window of step kLo without its newest row: rows rFirst .. rFirst + NT - 2 -> slots 0 .. NT - 2
+#pragma unroll
+    for (int i = 0; i < NT - 1; ++i)
+        widen(load_row(rFirst + i), R[i]);
+    // prefetch: step kLo + v adds row rFirst + NT - 1 + v (slot (v + NT - 1) % NW)
+    u32x2 pre[NW];
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+        __builtin_amdgcn_sched_barrier(0);
+        pre[v] = load_row(rFirst + NT - 1 + v);
+        // the loop's store pattern (two per step), dropped, so the header waits are steady-state
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, OOB + 32 * v, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, OOB + 32 * v + 16, 0);
+    }
+    for (int base = kLo; base < kHi; base += NW) {
+        static_for<NW>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int k = base + v;
+            __builtin_amdgcn_sched_barrier(0);
+            widen(pre[v], R[(v + NT - 1) % NW]);  // row k + OFF + NT - 1
+            pre[v] = load_row(k + NW + OFF + NT - 1);
+            uint32_t Wk[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)  // output row 2k: the source row k itself
+                Wk[q] = pk_mul(R[(v - OFF) % NW][q], u.cy0);
+            emit(Wk, 2 * k, 2 * k >= y0 && 2 * k < y1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // output row 2k + 1: rows k + OFF .. k + OFF + NT - 1
+                uint32_t acc = pk_mul(R[v % NW][q], u.cy1[0]);
+#pragma unroll
+                for (int i = 1; i < NT; ++i)
+                    acc = pk_mad(R[(v + i) % NW][q], u.cy1[i], acc);
+                Wk[q] = acc;
+            }
+            emit(Wk, 2 * k + 1, 2 * k + 1 >= y0 && 2 * k + 1 < y1);
+        });
+    }
+}
+
 // ================================================================ YUV 4:2:0 in one launch
 //
 // The three planes of a batch of I420 frames (the reference benchmark's workload,
@@ -2131,7 +2291,7 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
         return hipSuccess;
     const int rows = rowEnd - rowBegin;
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + t.srcW;
-    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + t.dstW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + t.dstW;  // stores are relative to dstRow0
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24) ||
         io.dstSt >= (int64_t(1) << 31) || t.srcH >= (1 << 24))
         return hipErrorInvalidValue;
@@ -2174,16 +2334,21 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
     return hipLaunchKernel(kern, grid, dim3(256), args, lds, s);
 }
 
-hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s,
+                       int stripLo, int strips, int stripStride)
 {
-    if (rowEnd <= rowBegin || io.frames <= 0)
+    if (strips < 0)
+        strips = w.nS;
+    if (rowEnd <= rowBegin || io.frames <= 0 || strips == 0)
         return hipSuccess;
+    if (stripLo < 0 || stripLo + (strips - 1) * stripStride >= w.nS || stripStride < 1)
+        return hipErrorInvalidValue;
     const int rows = rowEnd - rowBegin;
     const TileDev &t = w.t;
     // the buffer range ends at the dword holding the window's last pixel: a dword load that
     // crosses the range end reads as 0, and an aligned dword never crosses a page
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + ((t.srcW + 3) & ~3);
-    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + t.dstW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + t.dstW;  // stores are relative to dstRow0
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24))
         return hipErrorInvalidValue;
     const void *kern = nullptr;
@@ -2230,19 +2395,51 @@ hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd,
     // the latency of each wave's serial walk; MI355X G1/G2/G3 sweeps), bands of >= 16 rows
     if (bands <= 0) {
         const int64_t resident = std::max(1, resident_waves(kern, 256, lds));
-        const int64_t perBand = static_cast<int64_t>(w.nS) * io.frames;
+        const int64_t perBand = static_cast<int64_t>(strips) * io.frames;
         bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
     }
     bands = std::max(1, std::min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
-    const uint64_t nWaves = static_cast<uint64_t>(w.nS) * static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames);
+    const uint64_t nWaves = static_cast<uint64_t>(strips) * static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames);
     if (nWaves >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     WalkArgs a{w, io, rowBegin, rowEnd, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
-               static_cast<unsigned>(nWaves)};
+               static_cast<unsigned>(nWaves), stripLo, strips, stripStride};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, lds, s);
+}
+
+hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    const int rows = rowEnd - rowBegin;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + u.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + u.dstW;  // stores are relative to dstRow0
+    if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24) ||
+        (u.NT != 4 && u.NT != 6) || u.colLo < 16 || u.colHi > u.dstW - 16 || u.colLo >= u.colHi)
+        return hipErrorInvalidValue;
+    const void *kern = u.NT == 6 ? reinterpret_cast<const void *>(lanczos_up2_kernel<6>)
+                                 : reinterpret_cast<const void *>(lanczos_up2_kernel<4>);
+    const int wavesPerRow = (u.colHi - u.colLo + 991) / 992;
+    // bands: ~2.5 rounds of resident waves, at least 32 output rows (the window costs NT rows)
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
+        const int64_t perBand = static_cast<int64_t>(wavesPerRow) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 32)));
+    }
+    bands = std::max(1, std::min(bands, rows));
+    int rpb = (rows + bands - 1) / bands;
+    rpb += rpb & 1;  // even: a band's steps produce whole row pairs
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nWaves = static_cast<uint64_t>(wavesPerRow) * bands * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    Up2Args a{u, io, rowBegin, rowEnd, rpb, bands, wavesPerRow, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nWaves)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
 }
 
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)
@@ -2340,7 +2537,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;
-    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + l.dstW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + l.dstW;  // stores are relative to dstRow0
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 31) ||
         io.dstSt >= (int64_t(1) << 31))
         return hipErrorInvalidValue;
@@ -2422,7 +2619,7 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
     LinearArgs &a = P->a;
     a = LinearArgs{g, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, np};
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + g.srcW;
-    const int64_t db = static_cast<int64_t>(rows - 1) * io.dstSt + g.dstW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + g.dstW;  // stores are relative to dstRow0
     if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31))
         return hipErrorInvalidValue;
     a.srcBytes = static_cast<int>(sb);

@@ -60,7 +60,21 @@ struct WalkDev {
     const int4 *segs;            // 2 per row: {first, ring offset of first, border, first of row
                                  // + kWalkD}, {yM, yS, yNeg, 0} (plan.hpp WalkSeg; padded past the end)
 };
-hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+// strips stripLo + i * stripStride (i < strips; strips < 0: all of them)
+hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s,
+                       int stripLo = 0, int strips = -1, int stripStride = 1);
+
+// --- exact 2x Lanczos-2/3 upscale, main rows x middle columns (plan.hpp Up2Tables).
+struct Up2Dev {
+    int srcW, srcH, dstW, dstH;
+    int NT;                      // taps per axis (4 or 6)
+    int colLo, colHi;            // output columns written, [colLo, colHi)
+    uint32_t cy0;                // even rows: (c, c) splat of the single tap (the source row itself)
+    uint32_t cy1[6];             // odd rows: (c, c) splats of the NT taps
+    uint32_t cx0;                // even columns: (c, 0) of the single tap
+    uint32_t cx1[3];             // odd columns: int16 coefficient pairs of the NT taps
+};
+hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {

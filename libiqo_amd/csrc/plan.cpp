@@ -946,4 +946,76 @@ void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w)
     w->ok = true;
 }
 
+
+void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
+{
+    *u = Up2Tables();
+    if (p.method != kLanczos || !w.ok || p.x.identity || p.y.identity || p.dstW != 2 * p.srcW ||
+        p.dstH != 2 * p.srcH || w.nS < 3)
+        return;
+    const int NT = static_cast<int>(p.x.taps);
+    if ((NT != 4 && NT != 6) || static_cast<int>(p.y.taps) != NT)
+        return;
+    // a window is "main" if it is unmasked, NT wide, inside the source and starts where the
+    // kernel's fixed offset says; its coefficients must be the set of its parity, and the even set
+    // a single tap on the source sample itself
+    auto main_window = [&](const AxisPlan &ax, int i, bool isX, int len, std::vector<int32_t> (&set)[2]) {
+        const Window win = axis_window(p, ax, i, isX);
+        if (win.border || static_cast<int>(win.c.size()) != NT)
+            return false;
+        if (win.start != (i >> 1) + 1 - NT / 2 || win.start < 0 || win.start + NT > len)
+            return false;
+        std::vector<int32_t> &ref = set[i & 1];
+        if (ref.empty())
+            ref = win.c;
+        return ref == win.c;
+    };
+    std::vector<int32_t> ys[2], xs[2];
+    int m0 = -1, m1 = -1;
+    for (int y = 0; y < p.dstH; ++y) {
+        if (main_window(p.y, y, false, p.srcH, ys)) {
+            if (m0 < 0)
+                m0 = y;
+            else if (m1 >= 0)
+                return;  // main rows must be one contiguous run
+        } else if (m0 >= 0 && m1 < 0) {
+            m1 = y;
+        }
+    }
+    if (m0 < 0)
+        return;
+    if (m1 < 0)
+        m1 = p.dstH;
+    const int colLo = kWalkStrip, colHi = kWalkStrip * (w.nS - 1);
+    if (colHi <= colLo)
+        return;
+    for (int x = colLo; x < colHi; ++x)
+        if (!main_window(p.x, x, true, p.srcW, xs))
+            return;
+    if (m1 - m0 < 2 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
+        return;
+    auto single = [&](const std::vector<int32_t> &c) {
+        for (int i = 0; i < NT; ++i)
+            if ((i == NT / 2 - 1) != (c[static_cast<size_t>(i)] != 0))
+                return false;
+        return true;
+    };
+    if (!single(ys[0]) || !single(xs[0]))
+        return;
+    u->NT = NT;
+    u->m0 = m0;
+    u->m1 = m1;
+    u->colLo = colLo;
+    u->colHi = colHi;
+    auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
+    u->cy0 = splat(ys[0][static_cast<size_t>(NT / 2 - 1)]);
+    for (int i = 0; i < NT; ++i)
+        u->cy1[i] = splat(ys[1][static_cast<size_t>(i)]);
+    u->cx0 = static_cast<uint32_t>(xs[0][static_cast<size_t>(NT / 2 - 1)]) & 0xffffu;
+    for (int q = 0; q < NT / 2; ++q)
+        u->cx1[q] = (static_cast<uint32_t>(xs[1][static_cast<size_t>(2 * q)]) & 0xffffu) |
+                    (static_cast<uint32_t>(xs[1][static_cast<size_t>(2 * q + 1)]) << 16);
+    u->ok = true;
+}
+
 } // namespace iqo_amd

@@ -187,6 +187,21 @@ struct WalkTables {
 };
 void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w);
 
+// Exact 2x Lanczos upscale (kernels.hip lanczos_up2_kernel).  On the main rows and the middle
+// columns an even output y (x) is the source sample y/2 times one coefficient and an odd one
+// takes NT = 2 * degree taps starting at (y >> 1) + 1 - NT/2, one coefficient set per parity.
+// The kernel takes rows [m0, m1) x columns [colLo, colHi) ([256, 256 * (nS - 1)): whole walker
+// strips); the wave walker takes the rest.
+struct Up2Tables {
+    bool ok = false;
+    int NT = 0;
+    int m0 = 0, m1 = 0;
+    int colLo = 0, colHi = 0;
+    uint32_t cy0 = 0, cy1[6] = {};  // (c, c) u16 splats: even rows' single tap, odd rows' taps
+    uint32_t cx0 = 0, cx1[3] = {};  // (c, 0) / (c_2q, c_2q+1) int16 pairs for even / odd columns
+};
+void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u);
+
 // Build the full plan.  Returns false (with *err) for invalid arguments.
 bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                 size_t pxScale, Plan *out, std::string *err);

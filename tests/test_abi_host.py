@@ -100,7 +100,8 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 2, 640, 480, 320, 240, 1), "lanczos_stream"),
     (("area", 0, 7680, 4320, 1920, 1080, 1), "area_int"),
     (("linear", 0, 1920, 1080, 3840, 2160, 1), "linear_up2"),
-    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "walk"),          # general ratios: wave walker
+    (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "lanczos_up2"),   # exact 2x Lanczos: register-window streamer
+    (("lanczos", 3, 1921, 1080, 3842, 2160, 1), "walk"),          # general ratios: wave walker
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "walk"),
     (("area", 0, 1920, 1080, 1280, 720, 1), "walk"),
     (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),

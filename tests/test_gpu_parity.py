@@ -385,6 +385,7 @@ def test_tile_streamer_matches_oracle(cfg):
     t.set_option("walk", 0)
     assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    r.set_option("up2", 0)  # exact 2x Lanczos shapes: the walker alone (test_lanczos_up2_matches_oracle)
     kern = r.describe()["kernel"]
     assert kern in ("walk", "tile")
     src = torch.from_numpy(frames).to(DEV)
@@ -396,6 +397,7 @@ def test_tile_streamer_matches_oracle(cfg):
     if kern == "walk":
         for bands in (1, 3, 7, dh):
             w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+            w.set_option("up2", 0)
             w.set_option("bands", bands)
             out = w.resize_tensor(src).cpu().numpy()
             for f in range(2):
@@ -695,3 +697,52 @@ def test_concurrent_plans_from_host_threads(tmp_path):
         dst = np.fromfile(sp[:-4] + ".dst", np.uint8).reshape(dh, dw)
         m = ("lanczos", "area", "linear")[mi]
         assert (dst == ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)).all(), sp
+
+UP2_SHAPES = [
+    ("lanczos", 3, 1920, 1080, 3840, 2160, 1),   # G2
+    ("lanczos", 2, 960, 540, 1920, 1080, 1),
+    ("lanczos", 3, 640, 360, 1280, 720, 1),
+    ("lanczos", 3, 392, 100, 784, 200, 1),       # three strips: one 256-column middle strip
+]
+
+
+@pytest.mark.parametrize("cfg", UP2_SHAPES, ids=lambda c: "%s%d_%dx%d" % c[:4])
+def test_lanczos_up2_matches_oracle(cfg):
+    """Exact 2x Lanczos upscale: lanczos_up2_kernel on the main rows x middle columns, the wave
+    walker on the edge strips and border rows, equal to the oracle on noise and flat frames; with
+    option up2 = 0 (walker alone), in row bands (iqo_hip_resize_band windows), and with an
+    unaligned destination stride (walker alone)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    n = 2 if sw * sh > 1_000_000 else 3
+    frames = _noise_batch(n, sw, sh, 1300)
+    frames[-1] = 77
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert r.describe()["kernel"] == "lanczos_up2"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    w.set_option("up2", 0)
+    assert w.describe()["kernel"] == "walk"
+    assert (w.resize_tensor(src).cpu().numpy() == out).all()
+    for bands in (3, 7):
+        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option("bands", bands)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, "bands", bands)
+    # row bands through their source windows (odd band edges)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = [0, 3, dh // 3 + 1, dh // 2, dh]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    # destination stride not 16-byte aligned: the walker alone
+    dst = torch.zeros((n, dh, dw + 4), dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 4, dh * (dw + 4), dst.data_ptr())
+    torch.cuda.synchronize()
+    assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
