@@ -38,6 +38,7 @@ struct iqo_hip_plan {
     int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
                             // streamer, 2: per-wave symmetric streamer (all bit-identical)
     int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
+    int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
@@ -56,6 +57,9 @@ struct iqo_hip_plan {
     // exact 2x Lanczos upscale kernel on the main rows x middle columns (option "up2" = 0: walker only)
     iqo_amd::Up2Tables ut;
     bool useUp2 = true;
+    // exact 3:2 Lanczos-3 downscale kernel on the main rows (option "d32" = 0: walker only)
+    iqo_amd::D32Tables dt;
+    bool useD32 = true;
     int4 *dWSpans = nullptr;
     int4 *dWSegs = nullptr;
     uint32_t *dWRowTap = nullptr;
@@ -366,6 +370,7 @@ int upload_tile(iqo_hip_plan *h)
         if (rc)
             return rc;
         iqo_amd::build_up2(h->p, h->wt, &h->ut);
+        iqo_amd::build_d32(h->p, h->wt, &h->dt);
     }
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
@@ -475,6 +480,7 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.xNeg = f.xNeg;
     l.dbg = h->debugFlags;
     l.prefetch = h->prefetch;
+    l.ringPack = h->ringPack;
     l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
     l.NX = f.NX;
     l.offXO = f.offXO;
@@ -580,6 +586,22 @@ iqo_amd::Up2Dev up2_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::D32Tables &t = h->dt;
+    iqo_amd::D32Dev d;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.np = h->lanes;
+    std::memcpy(d.cy, t.cy, sizeof d.cy);
+    std::memcpy(d.cx, t.cx, sizeof d.cx);
+    std::memcpy(d.xM, t.xM, sizeof d.xM);
+    std::memcpy(d.xT, t.xT, sizeof d.xT);
+    return d;
+}
+
 iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
 {
     const Plan &p = h->p;
@@ -622,6 +644,9 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if (kernel == IQO_KERNEL_WALK && h->ut.ok && h->useUp2 && aligned(src, 8, srcSt, srcFrameSt) &&
         aligned(dst, 16, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_UP2;
+    // the 3:2 Lanczos kernel loads 12 B per lane (4-byte aligned) and stores 8 B per lane
+    if (kernel == IQO_KERNEL_WALK && h->dt.ok && h->useD32 && aligned(dst, 8, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_LANCZOS_D32;
     return kernel;
 }
 
@@ -704,6 +729,18 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             if (e == hipSuccess && std::max(rb, u.m1) < re)
                 e = iqo_amd::launch_walk(wd, io, std::max(rb, u.m1), re, h->bands, s, 1, nS - 2, 1);
         }
+        else if (kernel == IQO_KERNEL_LANCZOS_D32) {
+            // the walker takes the border rows (all strips); lanczos_d32_kernel the main rows
+            const iqo_amd::WalkDev wd = walk_dev(h);
+            const iqo_amd::D32Tables &t = h->dt;
+            const int f0 = std::max(rb, t.m0), f1 = std::min(re, t.m1);
+            if (rb < std::min(re, t.m0))
+                e = iqo_amd::launch_walk(wd, io, rb, std::min(re, t.m0), h->bands, s);
+            if (e == hipSuccess && f0 < f1)
+                e = iqo_amd::launch_d32(d32_dev(h), io, f0, f1, h->bands, s);
+            if (e == hipSuccess && std::max(rb, t.m1) < re)
+                e = iqo_amd::launch_walk(wd, io, std::max(rb, t.m1), re, h->bands, s);
+        }
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -767,7 +804,9 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->phasesY = h->p.y.phases;
     d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL
                                 : (h->p.kernel == IQO_KERNEL_GENERAL && h->tt.ok && h->useTile
-                                       ? (h->wt.ok && h->useWalk ? (h->ut.ok && h->useUp2 ? IQO_KERNEL_LANCZOS_UP2 : IQO_KERNEL_WALK)
+                                       ? (h->wt.ok && h->useWalk ? (h->ut.ok && h->useUp2   ? IQO_KERNEL_LANCZOS_UP2
+                                                                    : h->dt.ok && h->useD32 ? IQO_KERNEL_LANCZOS_D32
+                                                                                            : IQO_KERNEL_WALK)
                                                                  : IQO_KERNEL_TILE)
                                        : h->p.kernel);
     d->bandsPerFrame = h->bands;
@@ -788,6 +827,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
 #endif
+    if (!std::strcmp(key, "ring_pack")) {  // block-shared Lanczos streamer: packed ring rows (speed only)
+        h->ringPack = value != 0;
+        return IQO_HIP_OK;
+    }
     if (!std::strcmp(key, "xcd_order")) {  // block-shared Lanczos streamer workgroup order (A/B)
         h->xcdOrder = value != 0;
         return IQO_HIP_OK;
@@ -835,6 +878,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "up2")) {  // 0: exact 2x Lanczos upscales use the wave walker alone
         h->useUp2 = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "d32")) {  // 0: exact 3:2 Lanczos-3 downscales use the wave walker alone
+        h->useD32 = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "walk")) {  // 0: general ratios use tile_kernel instead of the wave walker
@@ -1345,7 +1392,8 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     if (!h.wt.ok || !h.useWalk)
         return IQO_KERNEL_TILE;
     iqo_amd::build_up2(h.p, h.wt, &h.ut);
-    return h.ut.ok && h.useUp2 ? IQO_KERNEL_LANCZOS_UP2 : IQO_KERNEL_WALK;
+    iqo_amd::build_d32(h.p, h.wt, &h.dt);
+    return h.ut.ok && h.useUp2 ? IQO_KERNEL_LANCZOS_UP2 : h.dt.ok && h.useD32 ? IQO_KERNEL_LANCZOS_D32 : IQO_KERNEL_WALK;
 }
 
 } // extern "C"

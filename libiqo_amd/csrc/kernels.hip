@@ -559,6 +559,7 @@ struct LanczosArgs {
     int np;                  // producing lanes per wave (symmetric streamer)
     int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
     int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
+    int lastLanes;           // block-shared streamer: lanes of the last DMA chunk (0 = all 64)
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -817,6 +818,20 @@ __device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_
                      : "=&s"(keep)
                      : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
                      : "memory");
+}
+
+// dma_row for the lanes of `mask` only (masked-off lanes write nothing to LDS): the last chunk of a
+// ring row DMAs just the bytes the row needs, so the ring rows can be packed tighter than 1 KiB
+__device__ __forceinline__ void dma_row_masked(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff,
+                                               uint64_t mask)
+{
+    uint32_t keep;
+    uint64_t save;
+    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %4, %5 offen nt lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+                 : "=&s"(keep), "=&s"(save)
+                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
+                 : "memory");
 }
 
 template <int N>
@@ -1095,12 +1110,18 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
     constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
     static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
-    // LDS: ring [K slots][2 rows][rowPitch] | edgeSum int4 [2][64] | 1 KiB DMA sink
+    // LDS: ring [K slots][2 rows][rowPitch] | edgeSum int4 [2][EDGE_BATCH] | 1 KiB DMA sink (only
+    // when some wave has fewer chunks than CPW)
+    constexpr int EB = IQO_SYMB_EDGE_BATCH;
+    static_assert((EB & (EB - 1)) == 0 && EB <= 64, "edge batch: power of two <= 64");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int rowPitch = a.rowPitch, slotBytes = 2 * rowPitch;
     uint8_t *const ring = lds;
-    int4 (*const edgeSum)[64] = reinterpret_cast<int4 (*)[64]>(lds + K * slotBytes);
-    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + 2 * 64 * 16);
+    int4 (*const edgeSum)[EB] = reinterpret_cast<int4 (*)[EB]>(lds + K * slotBytes);
+    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + 2 * EB * 16);
+    // the last chunk of a row DMAs only its first lastLanes lanes (the row's pitch ends there)
+    const int lastLanes = a.lastLanes > 0 && a.lastLanes < 64 ? a.lastLanes : 64;
+    const uint64_t lastMask = lastLanes == 64 ? ~0ull : (1ull << lastLanes) - 1ull;
 
     const LanczosDev &L = a.l;
     const int lane = static_cast<int>(threadIdx.x) & 63;
@@ -1167,8 +1188,13 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             const int v = (real && col < L.srcW && !(dbg & 2)) ? col : 0x7ff00000;
             const uint32_t d0 = real ? s + 16 + 1024 * c : ldsBase + sinkLds;
             const uint32_t d1 = real ? d0 + rowPitch : d0;
-            dma_row(d0, v, srcR, row_soff(r));
-            dma_row(d1, v, srcR, row_soff(r + dir));
+            if (real && c == a.chunks - 1 && lastLanes < 64) {  // uniform
+                dma_row_masked(d0, v, srcR, row_soff(r), lastMask);
+                dma_row_masked(d1, v, srcR, row_soff(r + dir), lastMask);
+            } else {
+                dma_row(d0, v, srcR, row_soff(r));
+                dma_row(d1, v, srcR, row_soff(r + dir));
+            }
         }
     };
     auto read_iter = [&](int i, uint4 &r0, uint4 &r1) {
@@ -1203,12 +1229,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         };
         const int rowOff = (yb + dir * lane - a.io.dstRow0) * dstSt;
         if (edgeL) {
-            const int4 e = edgeSum[0][lane & 63];
+            const int4 e = edgeSum[0][lane & (EB - 1)];
             const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
             __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff : 0x7ff00000, 0, 0);
         }
         if (edgeR) {
-            const int4 e = edgeSum[1][lane & 63];
+            const int4 e = edgeSum[1][lane & (EB - 1)];
             const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
             __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff + L.dstW - 4 : 0x7ff00000,
                                                   0, 0);
@@ -1382,12 +1408,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every 64 rows and at the band end one pass divides them, one row per lane
-            const int slot = i & (IQO_SYMB_EDGE_BATCH - 1);
+            const int slot = i & (EB - 1);
             if (edgeL && laneL)
                 edgeSum[0][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
             if (edgeR && laneR)
                 edgeSum[1][slot] = make_int4(sum[4], sum[5], sum[6], sum[7]);
-            if (slot == IQO_SYMB_EDGE_BATCH - 1 || i == nRows - 1) {
+            if (slot == EB - 1 || i == nRows - 1) {
                 __builtin_amdgcn_wave_barrier();
                 flush_edges(yy - dir * slot, slot + 1);  // after this row's main store (same addresses)
             }
@@ -2140,6 +2166,222 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     }
 }
 
+// ================================================================ exact 3:2 Lanczos-3 downscale
+//
+// Lanczos-3 at exactly 2/3 (e.g. 1920x1080 -> 1280x720; plan.cpp build_d32).  In the reference's
+// tables for this ratio output y takes the 10 taps of phase y & 1 starting at source row
+// 3 (y >> 1) - 4 + (y & 1) (IQOLanczosResizerImpl_Generic.cpp:144-190 tables, :404-454 row loop),
+// and the same for columns.  Rows come in groups m = (2m, 2m + 1) over the 10 source rows
+// 3m - 4 .. 3m + 5; the even row's non-zero taps are group rows 0..7, the odd row's 2..9, and each
+// group adds the 3 source rows 3m + 3 .. 3m + 5.  One WAVE per (row band, output strip, frame)
+// walks the band's groups top to bottom, no barrier:
+//
+// * lane l (1..np) owns output columns [x0 + 8(l-1), +8) and source columns [cb, cb + 12),
+//   cb = 3/2 x0 - 12 + 12 l; lanes 0 and np+1 are the halo.  Each source row is loaded once per
+//   band (12 B per lane, PD groups ahead, branch-free so the compiler's vm waits are exact) and
+//   widened to six u16 pairs in a register window of 12 rows (static names: 4 groups per trip).
+// * Vertical: 8 v_pk_mad_u16 per pair and output row (int16 wrap as the reference's work row).
+// * Horizontal: work columns cb - 4 .. cb + 15 (two pairs from each neighbour by DPP, odd-aligned
+//   pairs by v_alignbit); output j is 5 v_dot2_i32_i16 on pairs fixed at compile time.
+// * Border columns (masked, renormalised: :539-574) lie in the first / last lane of a row.  Source
+//   columns outside the image load as zero, so the dot products give the reference's masked
+//   numerators; the edge lane parks its 8 sums in LDS and once per trip (8 rows) lanes 0..7
+//   rewrite those 8 bytes of one row each with the exact division (host multiply-high constants,
+//   identity 2^20 for the lane's interior columns).
+// * Border rows stay with the wave walker (run_band).
+struct D32Args {
+    D32Dev d;
+    Io io;
+    int rowBegin, rowEnd;   // output rows of this launch (main rows)
+    int evenBegin;          // rowBegin & ~1: band b starts at evenBegin + b * rowsPerBand (even)
+    int rowsPerBand, bands, wavesPerRow, np;
+    int srcBytes, dstBytes;
+    unsigned nWaves;
+};
+
+template <int PD>
+__global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
+{
+    constexpr int NW = 12;     // register window rows: a group's 10 + the 2 the next group adds early
+    constexpr int U = NW / 3;  // groups per unrolled trip (window slots repeat)
+    constexpr int OOB = 0x7ff00000;
+    static_assert(U % PD == 0, "prefetch slots repeat within a trip");
+    const D32Dev &d = a.d;
+    __shared__ int4 park[4][2][8][2];  // per wave, side, row slot: the edge lane's 8 raw sums
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;  // whole wave; no barrier in this kernel
+    const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
+    const unsigned rest = gw / static_cast<unsigned>(a.wavesPerRow);
+    const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
+    const int yb = a.evenBegin + band * a.rowsPerBand;  // even: first row of group kLo
+    const int y0 = max(yb, a.rowBegin), y1 = min(yb + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int kLo = yb >> 1;
+    const int nG = (y1 - yb + 1) >> 1;  // groups of this band (dropped rows at either end)
+
+    const int opw = 8 * a.np;
+    const int x0 = max(0, min(wcol * opw, d.dstW - opw));
+    const int cb = (3 * x0) / 2 - 12 + 12 * lane;
+    const bool produce = lane >= 1 && lane <= a.np;
+    const int voff = (lane <= a.np + 1 && cb >= 0 && cb + 12 <= d.srcW) ? cb : OOB;
+    const int stoff = produce ? x0 + 8 * (lane - 1) : OOB;
+    const bool edgeL = x0 == 0, edgeR = x0 + opw >= d.dstW;  // wave holds border columns (uniform)
+    const bool laneL = edgeL && lane == 1, laneR = edgeR && lane == a.np;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+
+    // relative source row q = row rBase + q; rows of dropped outputs may lie outside the window:
+    // clamped (their values are never used); rows past the band's last group are not loaded.
+    // Out-of-range marks go in the (range-checked) VGPR offset.
+    const int rBase = 3 * kLo - 4;
+    const int rLast = 3 * (kLo + nG - 1) + 5;
+    const int srcLast = a.io.srcRowEnd - 1;
+    auto load_row = [&](int q) -> u32x3 {
+        const int r = rBase + q;
+        const int rc = min(max(r, srcRow0), srcLast);
+        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
+        P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
+        P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
+        P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
+        P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);
+        P[4] = __builtin_amdgcn_perm(0u, v.z, 0x0c010c00u);
+        P[5] = __builtin_amdgcn_perm(0u, v.z, 0x0c030c02u);  // (cb+10, cb+11)
+    };
+    auto store_row = [&](u32x2 o, int voffs, int y, bool ok) {
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+    };
+    // horizontal pass of one output row from the lane's six work pairs; the edge lane parks its sums
+    auto emit = [&](const uint32_t (&W)[6], int y, int slot) {
+        uint32_t E[10];  // E[e] = work columns (cb - 4 + 2e, cb - 3 + 2e)
+        E[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[4]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+        E[1] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[5]), 0x138, 0xf, 0xf, true));
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+            E[e + 2] = W[e];
+        E[8] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[0]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        E[9] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[1]), 0x130, 0xf, 0xf, true));
+        uint32_t O[9];  // O[e] = work columns (cb - 3 + 2e, cb - 2 + 2e)
+#pragma unroll
+        for (int e = 0; e < 9; ++e)
+            O[e] = __builtin_amdgcn_alignbit(E[e + 1], E[e], 16);
+        auto pair = [&](int rel) { return (rel & 1) ? O[(rel + 3) / 2] : E[(rel + 4) / 2]; };  // low half = column cb + rel
+        int sum[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int ph = j & 1;
+            const int rel = 3 * (j >> 1) - 4 + ph;  // window start of output x0 + 8(l-1) + j
+            int acc = sdot2(pair(rel), d.cx[ph][0], 1 << 19);
+#pragma unroll
+            for (int q = 1; q < 5; ++q)
+                acc = sdot2(pair(rel + 2 * q), d.cx[ph][q], acc);
+            sum[j] = acc;
+        }
+        u32x2 o;
+        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+        store_row(o, stoff, y, y >= y0 && y < y1);
+        if (edgeL || edgeR) {  // uniform
+            if (laneL || laneR) {
+                int4 *pk = park[wib][laneL ? 0 : 1][slot];
+                pk[0] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+                pk[1] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+            }
+        }
+    };
+    // once per trip: lane r < 8 rewrites the edge bytes of row yt + r from the parked sums
+    auto flush = [&](int yt) {
+        u32x2 oL = {0u, 0u}, oR = {0u, 0u};
+        if (edgeL || edgeR) {  // uniform
+            __builtin_amdgcn_wave_barrier();
+            auto fix = [&](int side) {
+                const int4 p0 = park[wib][side][lane & 7][0], p1 = park[wib][side][lane & 7][1];
+                const int sv[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+                uint32_t b[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    b[j] = min(__umulhi(static_cast<uint32_t>(max(sv[j], 0)), d.xM[side][j]) >> d.xT[side][j], 255u);
+                return u32x2{b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24), b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24)};
+            };
+            if (edgeL)
+                oL = fix(0);
+            if (edgeR)
+                oR = fix(1);
+        }
+        const int y = yt + lane;
+        const bool ok = lane < 8 && y >= y0 && y < y1;
+        store_row(oL, edgeL ? 0 : OOB, y, ok);
+        store_row(oR, edgeR ? d.dstW - 8 : OOB, y, ok);
+    };
+
+    uint32_t R[NW][6];
+    // the window of group 0 without the rows group 0 itself adds: relative rows 0..6 -> slots 0..6
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+        widen(load_row(q), R[q]);
+    // prefetch: group g adds relative rows 3g + 7 .. 3g + 9 (slots (3g + 7 .. 3g + 9) % NW)
+    u32x3 pre[PD][3];
+#pragma unroll
+    for (int v = 0; v < PD; ++v) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            pre[v][i] = load_row(3 * v + 7 + i);
+        // the loop's store pattern (two rows per group), dropped, so the header waits are steady-state
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
+    }
+    // and the trip's two flush stores
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
+    for (int base = 0; base < nG; base += U) {
+        static_for<U>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int g = base + v;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                widen(pre[v % PD][i], R[(3 * v + 7 + i) % NW]);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                pre[v % PD][i] = load_row(3 * (g + PD) + 7 + i);
+            const int y = 2 * (kLo + g);
+            uint32_t W[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = pk_mul(R[(3 * v) % NW][c], d.cy[0][0]);
+#pragma unroll
+            for (int t = 1; t < 8; ++t)
+#pragma unroll
+                for (int c = 0; c < 6; ++c)
+                    W[c] = pk_mad(R[(3 * v + t) % NW][c], d.cy[0][t], W[c]);
+            emit(W, y, 2 * v);
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = pk_mul(R[(3 * v + 2) % NW][c], d.cy[1][0]);
+#pragma unroll
+            for (int t = 1; t < 8; ++t)
+#pragma unroll
+                for (int c = 0; c < 6; ++c)
+                    W[c] = pk_mad(R[(3 * v + 2 + t) % NW][c], d.cy[1][t], W[c]);
+            emit(W, y + 1, 2 * v + 1);
+        });
+        flush(2 * (kLo + base));
+    }
+}
+
 // ================================================================ YUV 4:2:0 in one launch
 //
 // The three planes of a batch of I420 frames (the reference benchmark's workload,
@@ -2442,6 +2684,44 @@ hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, i
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
 }
 
+hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.dstW % 8 || d.dstW < 16 || 2 * d.srcW != 3 * d.dstW)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
+    const int lanes = d.dstW / 8;
+    int wpr = (lanes + 61) / 62;
+    int np = d.np > 0 ? min(d.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
+    const void *kern = reinterpret_cast<const void *>(lanczos_d32_kernel<2>);
+    const int evenBegin = rowBegin & ~1;
+    const int rows = rowEnd - evenBegin;
+    // bands: ~2.5 rounds of resident waves, whole trips (8 rows) per band, >= 16 rows
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
+        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
+    }
+    bands = std::max(1, std::min(bands, (rows + 7) / 8));
+    int rpb = (rows + bands - 1) / bands;
+    rpb = (rpb + 7) & ~7;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    D32Args a{d, io, rowBegin, rowEnd, evenBegin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nWaves)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
+}
+
+
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX)
 {
     return KY == 2 && KX == 2 &&
@@ -2482,21 +2762,28 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int pd = l.prefetch;
     const void *kern = nullptr;
     int block = 256, ldsBytes = 0;
-    const int chunks = (l.srcW + 16 + 1023) / 1024;
+    // block-shared ring rows: a 16-B zero pad, then LDS column 16 + c holds source column c.  A
+    // row must hold every source column and the right halo lane's 16 bytes past the last output
+    // pair (LDS bytes up to 32 + 2 dstW); it is DMA'd in 1-KiB chunks, the last one masked to
+    // the lanes the row needs, so the pitch is that extent and not a whole number of KiB
+    const int rowNeed = (std::max(32 + 2 * l.dstW, 16 + l.srcW) + 15) & ~15;
+    const int chunks = (rowNeed - 16 + 1023) / 1024;
+    const int lastLanes = (rowNeed - 16 - 1024 * (chunks - 1)) / 16;
     const int cpw = (chunks + wpr - 1) / wpr;
-    const int rowPitch = 16 + 1024 * chunks;
+    const int rowPitch = l.ringPack ? rowNeed : 16 + 1024 * chunks;
     const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
     if (shared) {
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
-        const int K = pd <= 2 ? 3 : 4;
-        ldsBytes = K * 2 * rowPitch + 2 * 64 * 16 + 1024;
+        const int K = pd <= 2 ? 3 : pd == 3 ? 4 : 5;
+        ldsBytes = K * 2 * rowPitch + 2 * IQO_SYMB_EDGE_BATCH * 16 + (cpw * wpr > chunks ? 1024 : 0);
         block = 64 * wpr;
+#define IQO_SYMB_K(NY_, NX_, OX_, K_, ONE_)                                                             \
+    (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 1, ONE_>)             \
+              : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 2, ONE_>))
 #define IQO_SYMB(NY_, NX_, OX_, ONE_)                                                                   \
-    (K == 3 ? (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 3, 1, ONE_>)  \
-                        : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 3, 2, ONE_>)) \
-            : (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 4, 1, ONE_>)  \
-                        : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, 4, 2, ONE_>)))
+    (K == 3 ? IQO_SYMB_K(NY_, NX_, OX_, 3, ONE_) : K == 4 ? IQO_SYMB_K(NY_, NX_, OX_, 4, ONE_)          \
+            : IQO_SYMB_K(NY_, NX_, OX_, 5, ONE_))
         if (l.NY == 10 && one)
             kern = IQO_SYMB(10, 12, -5, true);
         else if (l.NY == 10)
@@ -2504,6 +2791,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
         else
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB
+#undef IQO_SYMB_K
     } else if (l.sym) {
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         if (l.NY == 10 && one)
@@ -2533,7 +2821,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
-    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd};
+    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd,
+                    l.ringPack ? lastLanes : 64};
     // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;

@@ -76,6 +76,17 @@ struct Up2Dev {
 };
 hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
+// Exact 3:2 Lanczos-3 downscale (plan.hpp D32Tables): main rows x all columns.
+struct D32Dev {
+    int srcW, srcH, dstW, dstH;
+    int np;                      // producing lanes per wave (0 = auto)
+    uint32_t cy[2][8];           // (c, c) u16 splats: phase p's taps at group rows 2p .. 2p + 7
+    uint32_t cx[2][5];           // phase p's (c_2q, c_2q+1) int16 pairs
+    uint32_t xM[2][8];           // edge-lane exact divisions (left / right 8 columns)
+    int xT[2][8];
+};
+hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {
     int KY, KX, NY, NXP, offX;
@@ -97,6 +108,7 @@ struct LanczosDev {
     uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table
     int np;                      // producing lanes per wave (0 = auto)
     int xcd;                     // block-shared streamer: XCD-aware workgroup order (speed only)
+    int ringPack;                // block-shared streamer: ring rows packed to the bytes they need
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,

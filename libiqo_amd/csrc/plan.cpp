@@ -1018,4 +1018,87 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
     u->ok = true;
 }
 
+void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
+{
+    *d = D32Tables();
+    if (p.method != kLanczos || !w.ok || p.x.identity || p.y.identity || 2 * p.srcW != 3 * p.dstW ||
+        2 * p.srcH != 3 * p.dstH || p.dstW % 8 || p.dstW < 16 || p.dstH < 8)
+        return;
+    if (p.x.taps != 10 || p.y.taps != 10)
+        return;
+    auto start_ok = [](const Window &win, int i) { return win.start == 3 * (i >> 1) - 4 + (i & 1); };
+    auto phase_row = [](const AxisPlan &ax, int ph) {
+        return std::vector<int32_t>(ax.table.begin() + ph * ax.taps, ax.table.begin() + (ph + 1) * ax.taps);
+    };
+    // columns: every window (main or masked border) starts where the kernel's fixed offsets say and
+    // takes its parity's phase, so the kernel's unmasked sum over zero-padded work columns is the
+    // reference's masked numerator; border columns only among the 8 outermost on each side
+    std::vector<int32_t> xs[2];
+    for (int x = 0; x < p.dstW; ++x) {
+        const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
+        const Window win = axis_window(p, p.x, x, true);
+        if (!start_ok(win, x) || ci.tabOff % p.x.taps != 0)
+            return;
+        const std::vector<int32_t> c = phase_row(p.x, ci.tabOff / p.x.taps);
+        std::vector<int32_t> &ref = xs[x & 1];
+        if (ref.empty())
+            ref = c;
+        if (ref != c)
+            return;
+        const int side = x < 8 ? 0 : x >= p.dstW - 8 ? 1 : -1;
+        if (win.border && side < 0)
+            return;
+        if (side >= 0) {
+            const int j = side ? x - (p.dstW - 8) : x;
+            if (!magic_x(win.border ? win.div : (1 << 20), &d->xM[side][j], &d->xT[side][j]))
+                return;
+        }
+    }
+    // rows: one contiguous run of main rows with the fixed window starts and the two phases
+    std::vector<int32_t> ys[2];
+    int m0 = -1, m1 = -1;
+    for (int y = 0; y < p.dstH; ++y) {
+        const Window win = axis_window(p, p.y, y, false);
+        const bool main = !win.border && static_cast<int>(win.c.size()) == 10 && start_ok(win, y) &&
+                          win.start >= 0 && win.start + 10 <= p.srcH;
+        if (main) {
+            std::vector<int32_t> &ref = ys[y & 1];
+            if (ref.empty())
+                ref = win.c;
+            if (ref != win.c)
+                return;
+            if (m0 < 0)
+                m0 = y;
+            else if (m1 >= 0)
+                return;
+        } else if (m0 >= 0 && m1 < 0) {
+            m1 = y;
+        }
+    }
+    if (m0 < 0)
+        return;
+    if (m1 < 0)
+        m1 = p.dstH;
+    if (m1 - m0 < 8 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
+        return;
+    // group rows: the even row's tap t is group row t, the odd row's tap t group row t + 1; the
+    // kernel multiplies group rows 0..7 (even) and 2..9 (odd)
+    for (int t = 0; t < 10; ++t) {
+        if ((t >= 8 && ys[0][static_cast<size_t>(t)] != 0) || ((t < 1 || t > 8) && ys[1][static_cast<size_t>(t)] != 0))
+            return;
+    }
+    auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
+    for (int t = 0; t < 8; ++t) {
+        d->cy[0][t] = splat(ys[0][static_cast<size_t>(t)]);
+        d->cy[1][t] = splat(ys[1][static_cast<size_t>(t + 1)]);
+    }
+    for (int ph = 0; ph < 2; ++ph)
+        for (int q = 0; q < 5; ++q)
+            d->cx[ph][q] = (static_cast<uint32_t>(xs[ph][static_cast<size_t>(2 * q)]) & 0xffffu) |
+                           (static_cast<uint32_t>(xs[ph][static_cast<size_t>(2 * q + 1)]) << 16);
+    d->m0 = m0;
+    d->m1 = m1;
+    d->ok = true;
+}
+
 } // namespace iqo_amd

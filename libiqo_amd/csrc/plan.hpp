@@ -202,6 +202,22 @@ struct Up2Tables {
 };
 void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u);
 
+// Exact 3:2 Lanczos-3 downscale (kernels.hip lanczos_d32_kernel), e.g. 1920x1080 -> 1280x720.  In
+// the reference's tables for this ratio output y (x) takes the 10 taps of phase y & 1 starting at
+// 3 * (y >> 1) - 4 + (y & 1).  Output rows come in groups m (rows 2m, 2m+1) over the 10 source rows
+// 3m - 4 .. 3m + 5: the even row's non-zero taps are group rows 0..7, the odd row's 2..9.  The kernel
+// takes the main rows [m0, m1) x every column (the <= 8 border columns per side are divided in the
+// kernel); the wave walker takes the border rows.
+struct D32Tables {
+    bool ok = false;
+    int m0 = 0, m1 = 0;
+    uint32_t cy[2][8] = {};         // (c, c) u16 splats: phase p's taps at group rows 2p .. 2p + 7
+    uint32_t cx[2][5] = {};         // phase p's (c_2q, c_2q+1) int16 pairs from its window start
+    uint32_t xM[2][8] = {};         // edge lanes (left: columns 0..7, right: dstW - 8 .. dstW - 1):
+    int32_t xT[2][8] = {};          //   floor(s / D) = umulhi(s, xM) >> xT (D = 2^20 off the border)
+};
+void build_d32(const Plan &p, const WalkTables &w, D32Tables *d);
+
 // Build the full plan.  Returns false (with *err) for invalid arguments.
 bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                 size_t pxScale, Plan *out, std::string *err);

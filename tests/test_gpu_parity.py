@@ -746,3 +746,63 @@ def test_lanczos_up2_matches_oracle(cfg):
     r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 4, dh * (dw + 4), dst.data_ptr())
     torch.cuda.synchronize()
     assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+
+
+D32_SHAPES = [
+    ("lanczos", 3, 1920, 1080, 1280, 720, 1),    # G1: three waves per row (x0 of the last clamped)
+    ("lanczos", 3, 1440, 1080, 960, 720, 1),     # two waves per row
+    ("lanczos", 3, 504, 300, 336, 200, 1),       # one wave holding both edges
+]
+
+
+@pytest.mark.parametrize("cfg", D32_SHAPES, ids=lambda c: "%s%d_%dx%d" % c[:4])
+def test_lanczos_d32_matches_oracle(cfg):
+    """Exact 3:2 Lanczos-3 downscale: lanczos_d32_kernel on the main rows (border columns divided
+    in the kernel), the wave walker on the border rows; equal to the oracle on noise, flat and
+    half-flat frames; with option d32 = 0 (walker alone), in several band splits and lane counts,
+    in row bands through their source windows (odd band edges), with padded strides (d32 again)
+    and a destination stride that is not 8-byte aligned (walker alone)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    n = 3
+    frames = _noise_batch(n, sw, sh, 1700)
+    frames[1] = 77
+    frames[2, :, : sw // 2] = 255
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert r.describe()["kernel"] == "lanczos_d32"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    w.set_option("d32", 0)
+    assert w.describe()["kernel"] == "walk"
+    assert (w.resize_tensor(src).cpu().numpy() == out).all()
+    for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 8), ("lanes", 62)):
+        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option(opt, val)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
+    # row bands through their source windows (odd band edges)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = [0, 3, dh // 3 + 1, dh // 2, dh - 5, dh]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    # padded strides (4-byte aligned source rows, 8-byte aligned destination rows): d32 again
+    sst, dst_st = sw + 4, dw + 8
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 9, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
+    assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
+    # destination stride not 8-byte aligned: the walker alone
+    dst = torch.zeros((n, dh, dw + 4), dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 4, dh * (dw + 4), dst.data_ptr())
+    torch.cuda.synchronize()
+    assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
