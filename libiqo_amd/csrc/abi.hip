@@ -599,6 +599,10 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     std::memcpy(d.cx, t.cx, sizeof d.cx);
     std::memcpy(d.xM, t.xM, sizeof d.xM);
     std::memcpy(d.xT, t.xT, sizeof d.xT);
+    d.m0 = t.m0;
+    d.m1 = t.m1;
+    std::memcpy(d.yM, t.yM, sizeof d.yM);
+    std::memcpy(d.yS, t.yS, sizeof d.yS);
     return d;
 }
 
@@ -729,18 +733,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             if (e == hipSuccess && std::max(rb, u.m1) < re)
                 e = iqo_amd::launch_walk(wd, io, std::max(rb, u.m1), re, h->bands, s, 1, nS - 2, 1);
         }
-        else if (kernel == IQO_KERNEL_LANCZOS_D32) {
-            // the walker takes the border rows (all strips); lanczos_d32_kernel the main rows
-            const iqo_amd::WalkDev wd = walk_dev(h);
-            const iqo_amd::D32Tables &t = h->dt;
-            const int f0 = std::max(rb, t.m0), f1 = std::min(re, t.m1);
-            if (rb < std::min(re, t.m0))
-                e = iqo_amd::launch_walk(wd, io, rb, std::min(re, t.m0), h->bands, s);
-            if (e == hipSuccess && f0 < f1)
-                e = iqo_amd::launch_d32(d32_dev(h), io, f0, f1, h->bands, s);
-            if (e == hipSuccess && std::max(rb, t.m1) < re)
-                e = iqo_amd::launch_walk(wd, io, std::max(rb, t.m1), re, h->bands, s);
-        }
+        else if (kernel == IQO_KERNEL_LANCZOS_D32)
+            e = iqo_amd::launch_d32(d32_dev(h), io, rb, re, h->bands, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)

@@ -2188,7 +2188,9 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
 //   numerators; the edge lane parks its 8 sums in LDS and once per trip (8 rows) lanes 0..7
 //   rewrite those 8 bytes of one row each with the exact division (host multiply-high constants,
 //   identity 2^20 for the lane's interior columns).
-// * Border rows stay with the wave walker (run_band).
+// * Border rows (masked, renormalised: :464-490): source rows outside the image load as zero, so
+//   the window sum is the masked numerator; the row's work pairs are divided by its denominator
+//   (int16(n * 64 / deno), magic_y multiply-high) before the horizontal pass.
 struct D32Args {
     D32Dev d;
     Io io;
@@ -2241,16 +2243,18 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
 
-    // relative source row q = row rBase + q; rows of dropped outputs may lie outside the window:
-    // clamped (their values are never used); rows past the band's last group are not loaded.
-    // Out-of-range marks go in the (range-checked) VGPR offset.
+    // relative source row q = row rBase + q; rows outside the image read as zero (the masked
+    // border sums); rows of dropped outputs may lie outside the call's window: clamped (their
+    // values are never used); rows past the band's last group are not loaded.  Out-of-range marks
+    // go in the (range-checked) VGPR offset.
     const int rBase = 3 * kLo - 4;
     const int rLast = 3 * (kLo + nG - 1) + 5;
     const int srcLast = a.io.srcRowEnd - 1;
     auto load_row = [&](int q) -> u32x3 {
         const int r = rBase + q;
         const int rc = min(max(r, srcRow0), srcLast);
-        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+        const bool in = r >= 0 && r < d.srcH && r <= rLast;
+        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
     };
     auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
         P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
@@ -2326,6 +2330,18 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         store_row(oR, edgeR ? d.dstW - 8 : OOB, y, ok);
     };
 
+    // masked border row (uniform, rare): work = int16(n * 64 / deno)
+    auto border_row = [&](uint32_t (&W)[6], int y) {
+        if (y < d.m0 || y >= d.m1) {
+            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
+            const uint32_t m = d.yM[side][i];
+            const int sh = d.yS[side][i];
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = ydiv2(W[c], m, sh);
+        }
+    };
+
     uint32_t R[NW][6];
     // the window of group 0 without the rows group 0 itself adds: relative rows 0..6 -> slots 0..6
 #pragma unroll
@@ -2367,6 +2383,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
                     W[c] = pk_mad(R[(3 * v + t) % NW][c], d.cy[0][t], W[c]);
+            border_row(W, y);
             emit(W, y, 2 * v);
 #pragma unroll
             for (int c = 0; c < 6; ++c)
@@ -2376,6 +2393,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
                     W[c] = pk_mad(R[(3 * v + 2 + t) % NW][c], d.cy[1][t], W[c]);
+            border_row(W, y + 1);
             emit(W, y + 1, 2 * v + 1);
         });
         flush(2 * (kLo + base));

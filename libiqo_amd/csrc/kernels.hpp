@@ -84,6 +84,9 @@ struct D32Dev {
     uint32_t cx[2][5];           // phase p's (c_2q, c_2q+1) int16 pairs
     uint32_t xM[2][8];           // edge-lane exact divisions (left / right 8 columns)
     int xT[2][8];
+    int m0, m1;                  // main rows; the others are masked border rows divided by
+    uint32_t yM[2][8];           //   magic_y (top: row y, bottom: row y - m1)
+    int yS[2][8];
 };
 hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

@@ -1054,18 +1054,23 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
                 return;
         }
     }
-    // rows: one contiguous run of main rows with the fixed window starts and the two phases
+    // rows: the same fixed window starts and the two phases for every row; one contiguous run of
+    // main rows with at most 8 masked border rows above and below
     std::vector<int32_t> ys[2];
     int m0 = -1, m1 = -1;
     for (int y = 0; y < p.dstH; ++y) {
+        const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
         const Window win = axis_window(p, p.y, y, false);
-        const bool main = !win.border && static_cast<int>(win.c.size()) == 10 && start_ok(win, y) &&
-                          win.start >= 0 && win.start + 10 <= p.srcH;
-        if (main) {
-            std::vector<int32_t> &ref = ys[y & 1];
-            if (ref.empty())
-                ref = win.c;
-            if (ref != win.c)
+        if (!start_ok(win, y) || ci.tabOff % p.y.taps != 0)
+            return;
+        std::vector<int32_t> &ref = ys[y & 1];
+        const std::vector<int32_t> c = phase_row(p.y, ci.tabOff / p.y.taps);
+        if (ref.empty())
+            ref = c;
+        if (ref != c)
+            return;
+        if (!win.border) {
+            if (win.start < 0 || win.start + 10 > p.srcH)
                 return;
             if (m0 < 0)
                 m0 = y;
@@ -1079,8 +1084,16 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
         return;
     if (m1 < 0)
         m1 = p.dstH;
-    if (m1 - m0 < 8 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
+    if (m0 > 8 || p.dstH - m1 > 8 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
         return;
+    for (int y = 0; y < p.dstH; ++y) {
+        if (y >= m0 && y < m1)
+            continue;
+        const Window win = axis_window(p, p.y, y, false);
+        const int side = y < m0 ? 0 : 1, i = side ? y - m1 : y;
+        if (!win.border || !magic_y(win.div, &d->yM[side][i], &d->yS[side][i]))
+            return;
+    }
     // group rows: the even row's tap t is group row t, the odd row's tap t group row t + 1; the
     // kernel multiplies group rows 0..7 (even) and 2..9 (odd)
     for (int t = 0; t < 10; ++t) {

@@ -206,11 +206,14 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u);
 // the reference's tables for this ratio output y (x) takes the 10 taps of phase y & 1 starting at
 // 3 * (y >> 1) - 4 + (y & 1).  Output rows come in groups m (rows 2m, 2m+1) over the 10 source rows
 // 3m - 4 .. 3m + 5: the even row's non-zero taps are group rows 0..7, the odd row's 2..9.  The kernel
-// takes the main rows [m0, m1) x every column (the <= 8 border columns per side are divided in the
-// kernel); the wave walker takes the border rows.
+// takes every row and column: source rows / columns outside the image read as zero, so the masked
+// border numerators come out of the same sums, and the <= 8 border rows / columns per side are
+// divided in the kernel.
 struct D32Tables {
     bool ok = false;
-    int m0 = 0, m1 = 0;
+    int m0 = 0, m1 = 0;             // main rows; rows y < m0 and y >= m1 are masked border rows
+    uint32_t yM[2][8] = {};         // border row y (top: y, bottom: y - m1): int16(n * 64 / deno)
+    int32_t yS[2][8] = {};          //   by magic_y
     uint32_t cy[2][8] = {};         // (c, c) u16 splats: phase p's taps at group rows 2p .. 2p + 7
     uint32_t cx[2][5] = {};         // phase p's (c_2q, c_2q+1) int16 pairs from its window start
     uint32_t xM[2][8] = {};         // edge lanes (left: columns 0..7, right: dstW - 8 .. dstW - 1):

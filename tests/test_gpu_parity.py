@@ -757,8 +757,8 @@ D32_SHAPES = [
 
 @pytest.mark.parametrize("cfg", D32_SHAPES, ids=lambda c: "%s%d_%dx%d" % c[:4])
 def test_lanczos_d32_matches_oracle(cfg):
-    """Exact 3:2 Lanczos-3 downscale: lanczos_d32_kernel on the main rows (border columns divided
-    in the kernel), the wave walker on the border rows; equal to the oracle on noise, flat and
+    """Exact 3:2 Lanczos-3 downscale: lanczos_d32_kernel on every row and column (masked border
+    rows and columns divided in the kernel); equal to the oracle on noise, flat and
     half-flat frames; with option d32 = 0 (walker alone), in several band splits and lane counts,
     in row bands through their source windows (odd band edges), with padded strides (d32 again)
     and a destination stride that is not 8-byte aligned (walker alone)."""
