@@ -577,12 +577,17 @@ iqo_amd::Up2Dev up2_dev(const iqo_hip_plan *h)
     d.dstW = h->p.dstW;
     d.dstH = h->p.dstH;
     d.NT = u.NT;
-    d.colLo = u.colLo;
-    d.colHi = u.colHi;
+    d.np = h->lanes;
     d.cy0 = u.cy0;
     d.cx0 = u.cx0;
     std::memcpy(d.cy1, u.cy1, sizeof d.cy1);
     std::memcpy(d.cx1, u.cx1, sizeof d.cx1);
+    std::memcpy(d.xM, u.xM, sizeof d.xM);
+    std::memcpy(d.xT, u.xT, sizeof d.xT);
+    d.m0 = u.m0;
+    d.m1 = u.m1;
+    std::memcpy(d.yM, u.yM, sizeof d.yM);
+    std::memcpy(d.yS, u.yS, sizeof d.yS);
     return d;
 }
 
@@ -718,21 +723,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_tile(tile_dev(h), io, rb, re, s);
         else if (kernel == IQO_KERNEL_WALK)
             e = iqo_amd::launch_walk(walk_dev(h), io, rb, re, h->bands, s);
-        else if (kernel == IQO_KERNEL_LANCZOS_UP2) {
-            // the walker takes the two edge strips (all rows) and the border rows of the middle
-            // strips; lanczos_up2_kernel the main rows of the middle strips
-            const iqo_amd::WalkDev wd = walk_dev(h);
-            const iqo_amd::Up2Tables &u = h->ut;
-            const int nS = h->wt.nS;
-            const int f0 = std::max(rb, u.m0), f1 = std::min(re, u.m1);
-            e = iqo_amd::launch_walk(wd, io, rb, re, h->bands, s, 0, 2, nS - 1);
-            if (e == hipSuccess && rb < std::min(re, u.m0))
-                e = iqo_amd::launch_walk(wd, io, rb, std::min(re, u.m0), h->bands, s, 1, nS - 2, 1);
-            if (e == hipSuccess && f0 < f1)
-                e = iqo_amd::launch_up2(up2_dev(h), io, f0, f1, h->bands, s);
-            if (e == hipSuccess && std::max(rb, u.m1) < re)
-                e = iqo_amd::launch_walk(wd, io, std::max(rb, u.m1), re, h->bands, s, 1, nS - 2, 1);
-        }
+        else if (kernel == IQO_KERNEL_LANCZOS_UP2)
+            e = iqo_amd::launch_up2(up2_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_LANCZOS_D32)
             e = iqo_amd::launch_d32(d32_dev(h), io, rb, re, h->bands, s);
         else

@@ -2009,13 +2009,13 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 
 // ================================================================ exact 2x Lanczos upscale
 //
-// Lanczos-2/3 at exactly 2x (pxScale 1), main rows x middle columns (plan.cpp build_up2; the wave
-// walker does the edge strips and the border rows).  In the reference's tables for this ratio an
+// Lanczos-2/3 at exactly 2x (plan.cpp build_up2).  In the reference's tables for this ratio an
 // even output row / column sits exactly on a source sample (a single tap: 64 vertically, 2^14
 // horizontally) and an odd one takes NT = 2 * degree taps starting NT/2 - 1 samples to its left
-// (IQOLanczosResizerImpl_Generic.cpp:144-190, 404-454).  The linear_up2 streamer's layout: one
-// WAVE per (row band, 992-column output strip, frame) walks the band's SOURCE rows top to bottom;
-// lane l owns source columns [cb, cb + 8) and (lanes 1..62) output columns [2cb, 2cb + 16).
+// (IQOLanczosResizerImpl_Generic.cpp:144-190, 404-454), at the borders too (masked + renormalised,
+// :464-490, :539-574).  The linear_up2 streamer's layout: one WAVE per (row band, output strip,
+// frame) walks the band's SOURCE rows top to bottom; lane l (1..np) owns source columns
+// [cb, cb + 8) and output columns [2cb, 2cb + 16), lanes 0 and np+1 are the halo.
 //
 // Every source row is loaded once per band (8 B per lane, NT rows ahead) and widened to four u16
 // pairs in a register window of NT rows (static names: the loop is unrolled NT times).  Source
@@ -2025,11 +2025,18 @@ __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 // output 2cb + j is one (j even) or NT/2 (j odd) v_dot2_i32_i16 on pairs chosen at compile time.
 // Sixteen outputs pack into one 16-B store per lane.  Arithmetic as everywhere: int16-wrapping
 // vertical pass, (s + 2^19) >> 20 saturated to u8.
+//
+// Borders: source rows and columns outside the image load as zero, so the same sums are the
+// reference's masked numerators.  A border row's work pairs are divided by its denominator
+// (int16(n * 64 / deno), magic_y) before the horizontal pass; border columns lie in the first /
+// last lane of a row, which parks its 16 sums in LDS, and once per trip (2 NT rows) lanes
+// 0 .. 2NT-1 rewrite those 16 bytes of one row each with the exact division (magic_x constants,
+// identity 2^20 for the lane's interior columns).
 
 struct Up2Args {
     Up2Dev u;
     Io io;
-    int rowBegin, rowEnd, rowsPerBand, bands, wavesPerRow;
+    int rowBegin, rowEnd, rowsPerBand, bands, wavesPerRow, np;
     int srcBytes, dstBytes;
     unsigned nWaves;
 };
@@ -2042,6 +2049,7 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     constexpr int OFF = 1 - NT / 2;  // window start relative to x >> 1 (y >> 1)
     constexpr int OOB = 0x7ff00000;
     const Up2Dev &u = a.u;
+    __shared__ int4 park[4][2][2 * NW][4];  // per wave, side, row slot: the edge lane's 16 raw sums
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
@@ -2056,11 +2064,14 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     if (y0 >= y1)
         return;
 
-    const int xs0 = u.colLo / 2 + wcol * 62 * 8;  // first source column of lane 1
-    const int cb = xs0 - 8 + 8 * lane;
-    const bool produce = lane >= 1 && lane <= 62 && 2 * cb < u.colHi;
-    const int voff = cb + 8 <= u.srcW ? cb : OOB;  // the middle columns never need cb < 0
+    const int opw = 16 * a.np;
+    const int x0 = max(0, min(wcol * opw, u.dstW - opw));  // first output column of lane 1
+    const int cb = x0 / 2 - 8 + 8 * lane;
+    const bool produce = lane >= 1 && lane <= a.np;
+    const int voff = (lane <= a.np + 1 && cb >= 0 && cb + 8 <= u.srcW) ? cb : OOB;
     const int stoff = produce ? 2 * cb : OOB;
+    const bool edgeL = x0 == 0, edgeR = x0 + opw >= u.dstW;  // wave holds border columns (uniform)
+    const bool laneL = edgeL && lane == 1, laneR = edgeR && lane == a.np;
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
@@ -2071,15 +2082,17 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
 
     // source steps k: output rows 2k, 2k+1 (those outside [y0, y1) are computed and dropped);
-    // step k reads source rows k + OFF .. k + OFF + NT - 1
+    // step k reads source rows k + OFF .. k + OFF + NT - 1.  Rows outside the image read as zero
+    // (the masked border sums); rows of dropped outputs may lie outside the call's window: clamped
+    // (never used).  Out-of-range marks go in the (range-checked) VGPR offset.
     const int kLo = y0 >> 1, kHi = (y1 + 1) >> 1;
     const int rFirst = kLo + OFF;
     const int rLast = kHi - 1 + OFF + NT - 1;
-    // rows of dropped outputs may lie outside the window: clamped (their values are never used)
     const int srcLast = a.io.srcRowEnd - 1;
     auto load_row = [&](int r) -> u32x2 {
         const int rc = min(max(r, srcRow0), srcLast);
-        return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff, r <= rLast ? (rc - srcRow0) * srcSt : OOB, 0);
+        const bool in = r >= 0 && r < u.srcH && r <= rLast;
+        return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
     };
     auto widen = [&](u32x2 v, uint32_t (&P)[4]) {
         P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
@@ -2087,8 +2100,22 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
         P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
         P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);  // (cb+6, cb+7)
     };
+    auto store_row = [&](u32x4 o, int voffs, int y, bool ok) {
+        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+    };
+    // masked border row (uniform, rare): work = int16(n * 64 / deno)
+    auto border_row = [&](uint32_t (&W)[4], int y) {
+        if (y < u.m0 || y >= u.m1) {
+            const int side = y < u.m0 ? 0 : 1, i = min(max(side ? y - u.m1 : y, 0), 7);
+            const uint32_t m = u.yM[side][i];
+            const int sh = u.yS[side][i];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                W[q] = ydiv2(W[q], m, sh);
+        }
+    };
     // horizontal pass + store of output row y from the lane's four work pairs
-    auto emit = [&](const uint32_t (&Wk)[4], int y, bool valid) {
+    auto emit = [&](const uint32_t (&Wk)[4], int y, int slot) {
         uint32_t E[8];  // E[e] = work columns (cb - 4 + 2e, cb - 3 + 2e)
         E[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(Wk[2]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
         E[1] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(Wk[3]), 0x138, 0xf, 0xf, true));
@@ -2123,7 +2150,47 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
         o.z = pack_hi(pack_lo(sum[8], sum[9]), sum[10], sum[11]);
         o.w = pack_hi(pack_lo(sum[12], sum[13]), sum[14], sum[15]);
-        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, stoff, valid ? (y - dstRow0) * dstSt : OOB, 0);
+        store_row(o, stoff, y, y >= y0 && y < y1);
+        if (edgeL || edgeR) {  // uniform
+            if (laneL || laneR) {
+                int4 *pk = park[wib][laneL ? 0 : 1][slot];
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    pk[q] = make_int4(sum[4 * q], sum[4 * q + 1], sum[4 * q + 2], sum[4 * q + 3]);
+            }
+        }
+    };
+    // once per trip: lane r < 2 NW rewrites the edge bytes of row yt + r from the parked sums
+    auto flush = [&](int yt) {
+        u32x4 oL = {0u, 0u, 0u, 0u}, oR = {0u, 0u, 0u, 0u};
+        const int r = min(lane, 2 * NW - 1);
+        if (edgeL || edgeR) {  // uniform
+            __builtin_amdgcn_wave_barrier();
+            auto fix = [&](int side) {
+                uint32_t w[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int4 p = park[wib][side][r][q];
+                    const int sv[4] = {p.x, p.y, p.z, p.w};
+                    uint32_t b[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        b[e] = min(__umulhi(static_cast<uint32_t>(max(sv[e], 0)), u.xM[side][4 * q + e]) >>
+                                       u.xT[side][4 * q + e],
+                                   255u);
+                    w[q] = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+                }
+                return u32x4{w[0], w[1], w[2], w[3]};
+            };
+            if (edgeL)
+                oL = fix(0);
+            if (edgeR)
+                oR = fix(1);
+        }
+        const int y = yt + lane;
+        const bool ok = lane < 2 * NW && y >= y0 && y < y1;
+        store_row(oL, edgeL ? 0 : OOB, y, ok);
+        store_row(oR, edgeR ? u.dstW - 16 : OOB, y, ok);
     };
 
     uint32_t R[NW][4];
@@ -2138,9 +2205,12 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
         __builtin_amdgcn_sched_barrier(0);
         pre[v] = load_row(rFirst + NT - 1 + v);
         // the loop's store pattern (two per step), dropped, so the header waits are steady-state
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, OOB + 32 * v, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, OOB + 32 * v + 16, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
     }
+    // and the trip's two flush stores
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
     for (int base = kLo; base < kHi; base += NW) {
         static_for<NW>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
@@ -2152,7 +2222,8 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
 #pragma unroll
             for (int q = 0; q < 4; ++q)  // output row 2k: the source row k itself
                 Wk[q] = pk_mul(R[(v - OFF) % NW][q], u.cy0);
-            emit(Wk, 2 * k, 2 * k >= y0 && 2 * k < y1);
+            border_row(Wk, 2 * k);
+            emit(Wk, 2 * k, 2 * v);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {  // output row 2k + 1: rows k + OFF .. k + OFF + NT - 1
                 uint32_t acc = pk_mul(R[v % NW][q], u.cy1[0]);
@@ -2161,8 +2232,10 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
                     acc = pk_mad(R[(v + i) % NW][q], u.cy1[i], acc);
                 Wk[q] = acc;
             }
-            emit(Wk, 2 * k + 1, 2 * k + 1 >= y0 && 2 * k + 1 < y1);
+            border_row(Wk, 2 * k + 1);
+            emit(Wk, 2 * k + 1, 2 * v + 1);
         });
+        flush(2 * base);
     }
 }
 
@@ -2674,29 +2747,33 @@ hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, i
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    const int rows = rowEnd - rowBegin;
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + u.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + u.dstW;  // stores are relative to dstRow0
-    if (sb >= (int64_t(1) << 31) || db >= (int64_t(1) << 31) || io.srcSt >= (int64_t(1) << 24) ||
-        (u.NT != 4 && u.NT != 6) || u.colLo < 16 || u.colHi > u.dstW - 16 || u.colLo >= u.colHi)
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24) ||
+        (u.NT != 4 && u.NT != 6) || u.dstW % 16 || u.dstW != 2 * u.srcW || u.dstW < 32)
         return hipErrorInvalidValue;
     const void *kern = u.NT == 6 ? reinterpret_cast<const void *>(lanczos_up2_kernel<6>)
                                  : reinterpret_cast<const void *>(lanczos_up2_kernel<4>);
-    const int wavesPerRow = (u.colHi - u.colLo + 991) / 992;
+    // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
+    const int lanes = u.dstW / 16;
+    int wpr = (lanes + 61) / 62;
+    int np = u.np > 0 ? min(u.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
     // bands: ~2.5 rounds of resident waves, at least 32 output rows (the window costs NT rows)
     if (bands <= 0) {
         const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
-        const int64_t perBand = static_cast<int64_t>(wavesPerRow) * io.frames;
-        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 32)));
+        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, (rowEnd - rowBegin) / 32)));
     }
+    const int rows = rowEnd - rowBegin;
     bands = std::max(1, std::min(bands, rows));
     int rpb = (rows + bands - 1) / bands;
     rpb += rpb & 1;  // even: a band's steps produce whole row pairs
     bands = (rows + rpb - 1) / rpb;
-    const uint64_t nWaves = static_cast<uint64_t>(wavesPerRow) * bands * static_cast<uint64_t>(io.frames);
+    const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
     if (nWaves >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
-    Up2Args a{u, io, rowBegin, rowEnd, rpb, bands, wavesPerRow, static_cast<int>(sb), static_cast<int>(db),
+    Up2Args a{u, io, rowBegin, rowEnd, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nWaves)};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);

@@ -68,11 +68,16 @@ hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd,
 struct Up2Dev {
     int srcW, srcH, dstW, dstH;
     int NT;                      // taps per axis (4 or 6)
-    int colLo, colHi;            // output columns written, [colLo, colHi)
+    int np;                      // producing lanes per wave (0 = auto)
     uint32_t cy0;                // even rows: (c, c) splat of the single tap (the source row itself)
     uint32_t cy1[6];             // odd rows: (c, c) splats of the NT taps
     uint32_t cx0;                // even columns: (c, 0) of the single tap
     uint32_t cx1[3];             // odd columns: int16 coefficient pairs of the NT taps
+    uint32_t xM[2][16];          // edge-lane exact divisions (left / right 16 columns)
+    int xT[2][16];
+    int m0, m1;                  // main rows; the others are masked border rows divided by
+    uint32_t yM[2][8];           //   magic_y (top: row y, bottom: row y - m1)
+    int yS[2][8];
 };
 hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

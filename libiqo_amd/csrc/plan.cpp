@@ -951,29 +951,44 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
 {
     *u = Up2Tables();
     if (p.method != kLanczos || !w.ok || p.x.identity || p.y.identity || p.dstW != 2 * p.srcW ||
-        p.dstH != 2 * p.srcH || w.nS < 3)
+        p.dstH != 2 * p.srcH || p.dstW % 16 || p.dstW < 32 || p.dstH < 8)
         return;
     const int NT = static_cast<int>(p.x.taps);
     if ((NT != 4 && NT != 6) || static_cast<int>(p.y.taps) != NT)
         return;
-    // a window is "main" if it is unmasked, NT wide, inside the source and starts where the
-    // kernel's fixed offset says; its coefficients must be the set of its parity, and the even set
-    // a single tap on the source sample itself
-    auto main_window = [&](const AxisPlan &ax, int i, bool isX, int len, std::vector<int32_t> (&set)[2]) {
-        const Window win = axis_window(p, ax, i, isX);
-        if (win.border || static_cast<int>(win.c.size()) != NT)
+    // every window (main or masked border) starts where the kernel's fixed offset says and takes
+    // its parity's phase table, so the kernel's unmasked sums over zero-padded rows / columns are
+    // the reference's masked numerators
+    auto fixed = [&](const AxisPlan &ax, int i, std::vector<int32_t> (&set)[2]) {
+        const CoordInfo &ci = ax.coord[static_cast<size_t>(i)];
+        if (ci.kind == kIdentity || ci.srcO != (i >> 1) + 1 - NT / 2 || ci.tabOff % NT != 0)
             return false;
-        if (win.start != (i >> 1) + 1 - NT / 2 || win.start < 0 || win.start + NT > len)
-            return false;
+        const std::vector<int32_t> c(ax.table.begin() + ci.tabOff, ax.table.begin() + ci.tabOff + NT);
         std::vector<int32_t> &ref = set[i & 1];
         if (ref.empty())
-            ref = win.c;
-        return ref == win.c;
+            ref = c;
+        return ref == c;
     };
     std::vector<int32_t> ys[2], xs[2];
+    for (int x = 0; x < p.dstW; ++x) {
+        if (!fixed(p.x, x, xs))
+            return;
+        const Window win = axis_window(p, p.x, x, true);
+        const int side = x < 16 ? 0 : x >= p.dstW - 16 ? 1 : -1;
+        if (win.border && side < 0)
+            return;
+        if (side >= 0) {
+            const int j = side ? x - (p.dstW - 16) : x;
+            if (!magic_x(win.border ? win.div : (1 << 20), &u->xM[side][j], &u->xT[side][j]))
+                return;
+        }
+    }
     int m0 = -1, m1 = -1;
     for (int y = 0; y < p.dstH; ++y) {
-        if (main_window(p.y, y, false, p.srcH, ys)) {
+        if (!fixed(p.y, y, ys))
+            return;
+        const Window win = axis_window(p, p.y, y, false);
+        if (!win.border) {
             if (m0 < 0)
                 m0 = y;
             else if (m1 >= 0)
@@ -986,14 +1001,16 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
         return;
     if (m1 < 0)
         m1 = p.dstH;
-    const int colLo = kWalkStrip, colHi = kWalkStrip * (w.nS - 1);
-    if (colHi <= colLo)
+    if (m0 > 8 || p.dstH - m1 > 8 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
         return;
-    for (int x = colLo; x < colHi; ++x)
-        if (!main_window(p.x, x, true, p.srcW, xs))
+    for (int y = 0; y < p.dstH; ++y) {
+        if (y >= m0 && y < m1)
+            continue;
+        const Window win = axis_window(p, p.y, y, false);
+        const int side = y < m0 ? 0 : 1, i = side ? y - m1 : y;
+        if (!magic_y(win.div, &u->yM[side][i], &u->yS[side][i]))
             return;
-    if (m1 - m0 < 2 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
-        return;
+    }
     auto single = [&](const std::vector<int32_t> &c) {
         for (int i = 0; i < NT; ++i)
             if ((i == NT / 2 - 1) != (c[static_cast<size_t>(i)] != 0))
@@ -1005,8 +1022,6 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
     u->NT = NT;
     u->m0 = m0;
     u->m1 = m1;
-    u->colLo = colLo;
-    u->colHi = colHi;
     auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
     u->cy0 = splat(ys[0][static_cast<size_t>(NT / 2 - 1)]);
     for (int i = 0; i < NT; ++i)

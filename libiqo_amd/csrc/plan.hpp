@@ -187,16 +187,19 @@ struct WalkTables {
 };
 void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w);
 
-// Exact 2x Lanczos upscale (kernels.hip lanczos_up2_kernel).  On the main rows and the middle
-// columns an even output y (x) is the source sample y/2 times one coefficient and an odd one
-// takes NT = 2 * degree taps starting at (y >> 1) + 1 - NT/2, one coefficient set per parity.
-// The kernel takes rows [m0, m1) x columns [colLo, colHi) ([256, 256 * (nS - 1)): whole walker
-// strips); the wave walker takes the rest.
+// Exact 2x Lanczos upscale (kernels.hip lanczos_up2_kernel).  An even output y (x) is the source
+// sample y/2 times one coefficient and an odd one takes NT = 2 * degree taps starting at
+// (y >> 1) + 1 - NT/2, one coefficient set per parity, at the masked borders too.  The kernel takes
+// every row and column: source rows / columns outside the image read as zero, and the border rows
+// (<= 8 per side) and columns (<= 16 per side) are divided in the kernel.
 struct Up2Tables {
     bool ok = false;
     int NT = 0;
-    int m0 = 0, m1 = 0;
-    int colLo = 0, colHi = 0;
+    int m0 = 0, m1 = 0;             // main rows; the others are masked border rows
+    uint32_t xM[2][16] = {};        // edge lanes (left: columns 0..15, right: dstW - 16 ..):
+    int32_t xT[2][16] = {};         //   floor(s / D) = umulhi(s, xM) >> xT (D = 2^20 off the border)
+    uint32_t yM[2][8] = {};         // border row y (top: y, bottom: y - m1): int16(n * 64 / deno)
+    int32_t yS[2][8] = {};
     uint32_t cy0 = 0, cy1[6] = {};  // (c, c) u16 splats: even rows' single tap, odd rows' taps
     uint32_t cx0 = 0, cx1[3] = {};  // (c, 0) / (c_2q, c_2q+1) int16 pairs for even / odd columns
 };

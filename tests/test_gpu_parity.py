@@ -702,16 +702,17 @@ UP2_SHAPES = [
     ("lanczos", 3, 1920, 1080, 3840, 2160, 1),   # G2
     ("lanczos", 2, 960, 540, 1920, 1080, 1),
     ("lanczos", 3, 640, 360, 1280, 720, 1),
-    ("lanczos", 3, 392, 100, 784, 200, 1),       # three strips: one 256-column middle strip
+    ("lanczos", 3, 392, 100, 784, 200, 1),       # one wave holding both edges
+    ("lanczos", 2, 200, 60, 400, 120, 1),
 ]
 
 
 @pytest.mark.parametrize("cfg", UP2_SHAPES, ids=lambda c: "%s%d_%dx%d" % c[:4])
 def test_lanczos_up2_matches_oracle(cfg):
-    """Exact 2x Lanczos upscale: lanczos_up2_kernel on the main rows x middle columns, the wave
-    walker on the edge strips and border rows, equal to the oracle on noise and flat frames; with
-    option up2 = 0 (walker alone), in row bands (iqo_hip_resize_band windows), and with an
-    unaligned destination stride (walker alone)."""
+    """Exact 2x Lanczos upscale: lanczos_up2_kernel on every row and column (masked border rows
+    and columns divided in the kernel), equal to the oracle on noise and flat frames; with option
+    up2 = 0 (walker alone), in band splits and lane counts, in row bands (iqo_hip_resize_band
+    windows), and with an unaligned destination stride (walker alone)."""
     m, d, sw, sh, dw, dh, px = cfg
     n = 2 if sw * sh > 1_000_000 else 3
     frames = _noise_batch(n, sw, sh, 1300)
@@ -728,10 +729,10 @@ def test_lanczos_up2_matches_oracle(cfg):
     w.set_option("up2", 0)
     assert w.describe()["kernel"] == "walk"
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
-    for bands in (3, 7):
+    for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("lanes", 5), ("lanes", 62)):
         b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-        b.set_option("bands", bands)
-        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, "bands", bands)
+        b.set_option(opt, val)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
     # row bands through their source windows (odd band edges)
     got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
     cuts = [0, 3, dh // 3 + 1, dh // 2, dh]
