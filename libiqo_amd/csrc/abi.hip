@@ -60,6 +60,9 @@ struct iqo_hip_plan {
     // exact 3:2 Lanczos-3 downscale kernel on the main rows (option "d32" = 0: walker only)
     iqo_amd::D32Tables dt;
     bool useD32 = true;
+    // exact 3:2 Area downscale kernel (option "a32" = 0: walker only)
+    iqo_amd::A32Tables at;
+    bool useA32 = true;
     int4 *dWSpans = nullptr;
     int4 *dWSegs = nullptr;
     uint32_t *dWRowTap = nullptr;
@@ -372,6 +375,7 @@ int upload_tile(iqo_hip_plan *h)
         iqo_amd::build_up2(h->p, h->wt, &h->ut);
         iqo_amd::build_d32(h->p, h->wt, &h->dt);
     }
+    iqo_amd::build_a32(h->p, &h->at);
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
     for (size_t y = 0; y < t.rows.size(); ++y)
@@ -611,6 +615,19 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::A32Dev a32_dev(const iqo_hip_plan *h)
+{
+    iqo_amd::A32Dev d;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.np = h->lanes;
+    std::memcpy(d.cy, h->at.cy, sizeof d.cy);
+    std::memcpy(d.cx, h->at.cx, sizeof d.cx);
+    return d;
+}
+
 iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
 {
     const Plan &p = h->p;
@@ -629,6 +646,23 @@ iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
     g.nChunks = h->nChunks;
     g.ldsInts = h->ldsInts;
     return g;
+}
+
+// The kernel family a full-frame call with aligned pointers and strides runs.
+int plan_kernel(const iqo_hip_plan *h)
+{
+    int k = h->forceGeneral ? IQO_KERNEL_GENERAL : h->p.kernel;
+    if (k == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tt.ok && h->useTile)
+        k = IQO_KERNEL_TILE;
+    if (k == IQO_KERNEL_TILE && h->wt.ok && h->useWalk)
+        k = IQO_KERNEL_WALK;
+    if (k == IQO_KERNEL_WALK && h->ut.ok && h->useUp2)
+        k = IQO_KERNEL_LANCZOS_UP2;
+    if (k == IQO_KERNEL_WALK && h->dt.ok && h->useD32)
+        k = IQO_KERNEL_LANCZOS_D32;
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->at.ok && h->useA32)
+        k = IQO_KERNEL_AREA_D32;
+    return k;
 }
 
 // The kernel family a call with these pointers and strides runs: the plan's fast kernel when the
@@ -656,6 +690,9 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     // the 3:2 Lanczos kernel loads 12 B per lane (4-byte aligned) and stores 8 B per lane
     if (kernel == IQO_KERNEL_WALK && h->dt.ok && h->useD32 && aligned(dst, 8, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_D32;
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
+        aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_AREA_D32;
     return kernel;
 }
 
@@ -727,6 +764,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_up2(up2_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_LANCZOS_D32)
             e = iqo_amd::launch_d32(d32_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_AREA_D32)
+            e = iqo_amd::launch_a32(a32_dev(h), io, rb, re, h->bands, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -788,13 +827,7 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->tapsY = h->p.y.taps;
     d->phasesX = h->p.x.phases;
     d->phasesY = h->p.y.phases;
-    d->kernel = h->forceGeneral ? IQO_KERNEL_GENERAL
-                                : (h->p.kernel == IQO_KERNEL_GENERAL && h->tt.ok && h->useTile
-                                       ? (h->wt.ok && h->useWalk ? (h->ut.ok && h->useUp2   ? IQO_KERNEL_LANCZOS_UP2
-                                                                    : h->dt.ok && h->useD32 ? IQO_KERNEL_LANCZOS_D32
-                                                                                            : IQO_KERNEL_WALK)
-                                                                 : IQO_KERNEL_TILE)
-                                       : h->p.kernel);
+    d->kernel = plan_kernel(h);
     d->bandsPerFrame = h->bands;
     return IQO_HIP_OK;
 }
@@ -864,6 +897,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "up2")) {  // 0: exact 2x Lanczos upscales use the wave walker alone
         h->useUp2 = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "a32")) {  // 0: exact 3:2 Area downscales use the wave walker alone
+        h->useA32 = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "d32")) {  // 0: exact 3:2 Lanczos-3 downscales use the wave walker alone
@@ -1375,11 +1412,10 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     if (!h.tt.ok)
         return IQO_KERNEL_GENERAL;
     iqo_amd::build_walk_tables(h.p, h.tt, &h.wt);
-    if (!h.wt.ok || !h.useWalk)
-        return IQO_KERNEL_TILE;
     iqo_amd::build_up2(h.p, h.wt, &h.ut);
     iqo_amd::build_d32(h.p, h.wt, &h.dt);
-    return h.ut.ok && h.useUp2 ? IQO_KERNEL_LANCZOS_UP2 : h.dt.ok && h.useD32 ? IQO_KERNEL_LANCZOS_D32 : IQO_KERNEL_WALK;
+    iqo_amd::build_a32(h.p, &h.at);
+    return plan_kernel(&h);
 }
 
 } // extern "C"

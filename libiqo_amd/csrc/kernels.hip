@@ -2473,6 +2473,122 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     }
 }
 
+// ================================================================ exact 3:2 Area downscale
+//
+// Area at exactly 2/3 (plan.cpp build_a32; the reference's Area tables for this ratio,
+// IQOAreaResizerImpl_Generic.cpp:11-97, have two non-zero taps per phase): output rows 2m, 2m+1
+// read exactly source rows 3m .. 3m + 2 (171/85 and 85/171 of 256) and output columns
+// 8g .. 8g + 7 exactly source columns 12g .. 12g + 11, so a lane needs no neighbour and a row
+// pair no window.  One WAVE per (row band, 8 * np-column strip, frame); per row pair each lane
+// loads its 12 bytes of the 3 rows (PD pairs ahead), widens them to u16 pairs, forms the two u16
+// work rows (resizeYmain :313-319, 16-bit wrap) with packed MACs and the 8 outputs with one
+// v_dot2_u32_u16 each ((s + 2^22) >> 23, :349-367), one 8-byte store per row.
+struct A32Args {
+    A32Dev d;
+    Io io;
+    int rowBegin, rowEnd, evenBegin, rowsPerBand, bands, wavesPerRow, np;
+    int srcBytes, dstBytes;
+    unsigned nWaves;
+};
+
+template <int PD>
+__global__ __launch_bounds__(256) void area_d32_kernel(A32Args a)
+{
+    constexpr int OOB = 0x7ff00000;
+    const A32Dev &d = a.d;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;
+    const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
+    const unsigned rest = gw / static_cast<unsigned>(a.wavesPerRow);
+    const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
+    const int yb = a.evenBegin + band * a.rowsPerBand;  // even
+    const int y0 = max(yb, a.rowBegin), y1 = min(yb + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int kLo = yb >> 1;
+    const int nG = (y1 - yb + 1) >> 1;
+
+    const int opw = 8 * a.np;
+    const int x0 = max(0, min(wcol * opw, d.dstW - opw));
+    const bool produce = lane < a.np;
+    const int voff = produce ? (3 * x0) / 2 + 12 * lane : OOB;
+    const int stoff = produce ? x0 + 8 * lane : OOB;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+    const int rLast = 3 * (kLo + nG) - 1;
+    const int srcLast = a.io.srcRowEnd - 1;
+    // source row r (group rows of dropped outputs may lie outside the call's window: clamped, never
+    // used; rows past the band's last group are not loaded)
+    auto load_row = [&](int r) -> u32x3 {
+        const int rc = min(max(r, srcRow0), srcLast);
+        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
+        P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);
+        P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
+        P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
+        P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);
+        P[4] = __builtin_amdgcn_perm(0u, v.z, 0x0c010c00u);
+        P[5] = __builtin_amdgcn_perm(0u, v.z, 0x0c030c02u);
+    };
+    auto emit = [&](const uint32_t (&E)[6], int y) {
+        // output j: pair at column 3 (j >> 1) + (j & 1): E[k] = (2k, 2k+1), odd starts by alignbit
+        const uint32_t O1 = __builtin_amdgcn_alignbit(E[1], E[0], 16), O3 = __builtin_amdgcn_alignbit(E[2], E[1], 16);
+        const uint32_t O7 = __builtin_amdgcn_alignbit(E[4], E[3], 16), O9 = __builtin_amdgcn_alignbit(E[5], E[4], 16);
+        const uint32_t b = 1u << 22;
+        u32x2 o;
+        o.x = pack23_hi(pack23_lo(udot2(E[0], d.cx[0], b), udot2(O1, d.cx[1], b)), udot2(O3, d.cx[0], b),
+                        udot2(E[2], d.cx[1], b));
+        o.y = pack23_hi(pack23_lo(udot2(E[3], d.cx[0], b), udot2(O7, d.cx[1], b)), udot2(O9, d.cx[0], b),
+                        udot2(E[5], d.cx[1], b));
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff + (y >= y0 && y < y1 ? (y - dstRow0) * dstSt : OOB), 0, 0);
+    };
+
+    u32x3 pre[PD][3];
+#pragma unroll
+    for (int v = 0; v < PD; ++v) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            pre[v][i] = load_row(3 * (kLo + v) + i);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
+    }
+    for (int base = 0; base < nG; base += PD) {
+        static_for<PD>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int g = base + v;
+            __builtin_amdgcn_sched_barrier(0);
+            uint32_t A[6], B[6], C[6];
+            widen(pre[v][0], A);
+            widen(pre[v][1], B);
+            widen(pre[v][2], C);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                pre[v][i] = load_row(3 * (kLo + g + PD) + i);
+            uint32_t W[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = pk_mad(B[c], d.cy[0][1], pk_mul(A[c], d.cy[0][0]));
+            emit(W, 2 * (kLo + g));
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = pk_mad(C[c], d.cy[1][1], pk_mul(B[c], d.cy[1][0]));
+            emit(W, 2 * (kLo + g) + 1);
+        });
+    }
+}
+
 // ================================================================ YUV 4:2:0 in one launch
 //
 // The three planes of a batch of I420 frames (the reference benchmark's workload,
@@ -2811,6 +2927,42 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     if (nWaves >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     D32Args a{d, io, rowBegin, rowEnd, evenBegin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nWaves)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
+}
+
+hipError_t launch_a32(const A32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.dstW % 8 || d.dstW < 8 || 2 * d.srcW != 3 * d.dstW)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    const int lanes = d.dstW / 8;
+    int wpr = (lanes + 63) / 64;
+    int np = d.np > 0 ? min(d.np, min(64, lanes)) : (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
+    const void *kern = reinterpret_cast<const void *>(area_d32_kernel<4>);
+    const int evenBegin = rowBegin & ~1;
+    const int rows = rowEnd - evenBegin;
+    // bands: ~2.5 rounds of resident waves, whole trips (2 PD rows) per band, >= 16 rows
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
+        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
+    }
+    bands = std::max(1, std::min(bands, (rows + 7) / 8));
+    int rpb = (rows + bands - 1) / bands;
+    rpb = (rpb + 7) & ~7;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    A32Args a{d, io, rowBegin, rowEnd, evenBegin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nWaves)};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);

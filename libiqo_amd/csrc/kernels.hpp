@@ -95,6 +95,15 @@ struct D32Dev {
 };
 hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
+// Exact 3:2 Area downscale (plan.hpp A32Tables).
+struct A32Dev {
+    int srcW, srcH, dstW, dstH;
+    int np;                      // producing lanes per wave (0 = auto)
+    uint32_t cy[2][2];           // (c, c) u16 splats of phase p's two taps
+    uint32_t cx[2];              // phase p's (c_0, c_1) u16 pair
+};
+hipError_t launch_a32(const A32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
 // --- Lanczos row-band streamer (integer ratio, single phase).
 struct LanczosDev {
     int KY, KX, NY, NXP, offX;

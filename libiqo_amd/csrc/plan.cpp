@@ -1033,6 +1033,41 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
     u->ok = true;
 }
 
+void build_a32(const Plan &p, A32Tables *t)
+{
+    *t = A32Tables();
+    if (p.method != kArea || p.x.identity || p.y.identity || 2 * p.srcW != 3 * p.dstW || 2 * p.srcH != 3 * p.dstH ||
+        p.dstW % 8 || p.dstW < 8 || p.dstH < 2 || p.x.taps < 2 || p.y.taps < 2)
+        return;
+    // every coordinate: the fixed start, its parity's phase, no non-zero tap past the second
+    auto axis = [&](const AxisPlan &ax, std::vector<int32_t> (&set)[2]) {
+        for (int i = 0; i < ax.dstLen; ++i) {
+            const CoordInfo &ci = ax.coord[static_cast<size_t>(i)];
+            if (ci.kind != kMain || ci.srcO != 3 * (i >> 1) + (i & 1) || ci.tabOff % ax.taps != 0)
+                return false;
+            const std::vector<int32_t> c(ax.table.begin() + ci.tabOff, ax.table.begin() + ci.tabOff + ax.taps);
+            for (size_t k = 2; k < c.size(); ++k)
+                if (c[k] != 0)
+                    return false;
+            std::vector<int32_t> &ref = set[i & 1];
+            if (ref.empty())
+                ref = c;
+            if (ref != c)
+                return false;
+        }
+        return !set[0].empty() && !set[1].empty();
+    };
+    std::vector<int32_t> xs[2], ys[2];
+    if (!axis(p.x, xs) || !axis(p.y, ys))
+        return;
+    for (int ph = 0; ph < 2; ++ph) {
+        for (int k = 0; k < 2; ++k)
+            t->cy[ph][k] = (static_cast<uint32_t>(ys[ph][static_cast<size_t>(k)]) & 0xffffu) * 0x10001u;
+        t->cx[ph] = (static_cast<uint32_t>(xs[ph][0]) & 0xffffu) | (static_cast<uint32_t>(xs[ph][1]) << 16);
+    }
+    t->ok = true;
+}
+
 void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
 {
     *d = D32Tables();

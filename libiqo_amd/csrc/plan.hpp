@@ -224,6 +224,17 @@ struct D32Tables {
 };
 void build_d32(const Plan &p, const WalkTables &w, D32Tables *d);
 
+// Exact 3:2 Area downscale (kernels.hip area_d32_kernel), e.g. 1920x1080 -> 1280x720: output y (x)
+// takes the 2 non-zero taps of phase y & 1 starting at 3 (y >> 1) + (y & 1) (the third tap of the
+// reference's table is 0), so a row pair reads exactly the 3 source rows 3m .. 3m + 2 and a lane's
+// 8 outputs exactly its own 12 source columns.
+struct A32Tables {
+    bool ok = false;
+    uint32_t cy[2][2] = {};         // (c, c) u16 splats of phase p's two taps
+    uint32_t cx[2] = {};            // phase p's (c_0, c_1) u16 pair
+};
+void build_a32(const Plan &p, A32Tables *t);
+
 // Build the full plan.  Returns false (with *err) for invalid arguments.
 bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                 size_t pxScale, Plan *out, std::string *err);

@@ -52,6 +52,7 @@ def test_golden_vectors_gpu(golden, variant):
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
         if variant == "tile":
             r.set_option("walk", 0)
+            r.set_option("a32", 0)
         elif variant != "default":
             r.set_option(variant, 1)
         src = ol.gen(c["gen"], sw, sh, c["seed"])
@@ -383,9 +384,11 @@ def test_tile_streamer_matches_oracle(cfg):
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
     t = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
     t.set_option("walk", 0)
+    t.set_option("a32", 0)
     assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    r.set_option("up2", 0)  # exact 2x Lanczos shapes: the walker alone (test_lanczos_up2_matches_oracle)
+    for k in ("up2", "d32", "a32"):  # exact-ratio kernels off: the walker alone (their own tests below)
+        r.set_option(k, 0)
     kern = r.describe()["kernel"]
     assert kern in ("walk", "tile")
     src = torch.from_numpy(frames).to(DEV)
@@ -397,7 +400,8 @@ def test_tile_streamer_matches_oracle(cfg):
     if kern == "walk":
         for bands in (1, 3, 7, dh):
             w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-            w.set_option("up2", 0)
+            for k in ("up2", "d32", "a32"):
+                w.set_option(k, 0)
             w.set_option("bands", bands)
             out = w.resize_tensor(src).cpu().numpy()
             for f in range(2):
@@ -803,6 +807,63 @@ def test_lanczos_d32_matches_oracle(cfg):
     assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
     assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
     # destination stride not 8-byte aligned: the walker alone
+    dst = torch.zeros((n, dh, dw + 4), dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 4, dh * (dw + 4), dst.data_ptr())
+    torch.cuda.synchronize()
+    assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+
+
+A32_SHAPES = [
+    ("area", 0, 1920, 1080, 1280, 720, 1),       # G3: three waves per row (x0 of the last clamped)
+    ("area", 0, 504, 300, 336, 200, 1),          # one wave per row
+    ("area", 0, 48, 30, 32, 20, 1),
+    ("area", 0, 12, 6, 8, 4, 1),                 # one lane per row
+]
+
+
+@pytest.mark.parametrize("cfg", A32_SHAPES, ids=lambda c: "%s_%dx%d" % (c[0], c[2], c[3]))
+def test_area_d32_matches_oracle(cfg):
+    """Exact 3:2 Area downscale: area_d32_kernel equal to the oracle on noise, flat and half-flat
+    frames; with option a32 = 0 (walker or tile kernel), in band splits and lane counts, in row
+    bands through their source windows, with padded strides (a32 again) and a destination stride
+    that is not 8-byte aligned (walker / tile)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    n = 3
+    frames = _noise_batch(n, sw, sh, 1900)
+    frames[1] = 255
+    frames[2, :, : sw // 2] = 0
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert r.describe()["kernel"] == "area_d32"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    w.set_option("a32", 0)
+    assert w.describe()["kernel"] in ("walk", "tile")
+    assert (w.resize_tensor(src).cpu().numpy() == out).all()
+    for opt, val in (("bands", 1), ("bands", 3), ("bands", dh), ("lanes", 1), ("lanes", 7)):
+        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option(opt, val)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = sorted({0, 1, dh // 3 + 1, dh // 2, dh})
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    sst, dst_st = sw + 4, dw + 8
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 9, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
+    assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
     dst = torch.zeros((n, dh, dw + 4), dtype=torch.uint8, device=DEV)
     r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 4, dh * (dw + 4), dst.data_ptr())
     torch.cuda.synchronize()
