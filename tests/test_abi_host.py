@@ -103,7 +103,9 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "lanczos_up2"),   # exact 2x Lanczos: register-window streamer
     (("lanczos", 3, 1921, 1080, 3842, 2160, 1), "walk"),          # general ratios: wave walker
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "walk"),
-    (("area", 0, 1920, 1080, 1280, 720, 1), "walk"),
+    (("area", 0, 1920, 1080, 1280, 720, 1), "area_d32"),          # exact 3:2 Area: no window, no halo
+    (("lanczos", 3, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-3: register window
+    (("area", 0, 1921, 1080, 1280, 720, 1), "walk"),
     (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),
     (("lanczos", 3, 13, 9, 5, 40, 1), "tile"),                    # 13 columns: no 256-column strip fits the walker's tables
     (("lanczos", 9, 64, 48, 1000, 900, 1), "tile"),               # 64 work columns per row window: tiles
