@@ -19,9 +19,10 @@ import sys
 
 KERNELS = {"lanczos_stream": "lanczos_s", "area_int": "area_int_kernel",  # lanczos_s: symb / sym / stream
            "linear_up2": "linear_up2_kernel", "general": "general_kernel", "tile": "tile_kernel",
-           "walk": "walk_kernel"}
+           "walk": "walk_kernel", "lanczos_up2": "lanczos_up2_kernel", "lanczos_d32": "lanczos_d32_kernel",
+           "area_d32": "area_d32_kernel"}
 BENCH = {"c2": ("lanczos_stream", 128), "c3": ("area_int", 64), "c4": ("linear_up2", 256), "c1": ("lanczos_stream", 4096),
-         "g1": ("walk", 128), "g2": ("walk", 32), "g3": ("walk", 128)}
+         "g1": ("lanczos_d32", 128), "g2": ("lanczos_up2", 32), "g3": ("area_d32", 128)}
 
 
 def per_dispatch(dirname, counter, kname):
