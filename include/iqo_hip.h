@@ -91,7 +91,8 @@ int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
  * IQO_KERNEL_WALK / _LANCZOS_UP2; default 1), "up2" (0: IQO_KERNEL_WALK instead of
  * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" (0: IQO_KERNEL_WALK instead of
  * IQO_KERNEL_LANCZOS_D32 / IQO_KERNEL_AREA_D32; default 1), "tile_rows" (output rows per tile, 0 = auto),
- * "prefetch", "lin_prefetch", "stream_variant", "lanes", "chunk_frames", "xcd_order" (A/B of
+ * "prefetch", "lin_prefetch", "ratio_prefetch", "ring_pack", "stream_variant", "lanes",
+ * "chunk_frames", "xcd_order" (A/B of
  * kernel variants and schedules, see libiqo_amd/csrc/abi.hip).  Every option changes speed only,
  * never the output bytes.  IQO_HIP_EINVAL for an unknown key or value. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);

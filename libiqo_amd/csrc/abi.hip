@@ -40,6 +40,7 @@ struct iqo_hip_plan {
     int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
+    int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
     // it off, leaving general_kernel)
@@ -604,6 +605,7 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     d.dstW = h->p.dstW;
     d.dstH = h->p.dstH;
     d.np = h->lanes;
+    d.pd = h->ratioPrefetch;
     std::memcpy(d.cy, t.cy, sizeof d.cy);
     std::memcpy(d.cx, t.cx, sizeof d.cx);
     std::memcpy(d.xM, t.xM, sizeof d.xM);
@@ -623,6 +625,7 @@ iqo_amd::A32Dev a32_dev(const iqo_hip_plan *h)
     d.dstW = h->p.dstW;
     d.dstH = h->p.dstH;
     d.np = h->lanes;
+    d.pd = h->ratioPrefetch;
     std::memcpy(d.cy, h->at.cy, sizeof d.cy);
     std::memcpy(d.cx, h->at.cx, sizeof d.cx);
     return d;
@@ -901,6 +904,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "a32")) {  // 0: exact 3:2 Area downscales use the wave walker alone
         h->useA32 = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ratio_prefetch")) {  // exact 3:2 kernels: row groups loaded ahead (speed only)
+        if (value < 0 || value > 8)
+            return IQO_HIP_EINVAL;
+        h->ratioPrefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "d32")) {  // 0: exact 3:2 Lanczos-3 downscales use the wave walker alone

@@ -2910,7 +2910,10 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     int wpr = (lanes + 61) / 62;
     int np = d.np > 0 ? min(d.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
-    const void *kern = reinterpret_cast<const void *>(lanczos_d32_kernel<2>);
+    // one group of rows loaded ahead by default (G1, fresh data: 2.5 % faster than 2, 8 % than 4)
+    const void *kern = d.pd == 2   ? reinterpret_cast<const void *>(lanczos_d32_kernel<2>)
+                       : d.pd == 4 ? reinterpret_cast<const void *>(lanczos_d32_kernel<4>)
+                                   : reinterpret_cast<const void *>(lanczos_d32_kernel<1>);
     const int evenBegin = rowBegin & ~1;
     const int rows = rowEnd - evenBegin;
     // bands: ~2.5 rounds of resident waves, whole trips (8 rows) per band, >= 16 rows
@@ -2946,7 +2949,9 @@ hipError_t launch_a32(const A32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     int wpr = (lanes + 63) / 64;
     int np = d.np > 0 ? min(d.np, min(64, lanes)) : (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
-    const void *kern = reinterpret_cast<const void *>(area_d32_kernel<4>);
+    const void *kern = d.pd == 2   ? reinterpret_cast<const void *>(area_d32_kernel<2>)
+                       : d.pd == 8 ? reinterpret_cast<const void *>(area_d32_kernel<8>)
+                                   : reinterpret_cast<const void *>(area_d32_kernel<4>);
     const int evenBegin = rowBegin & ~1;
     const int rows = rowEnd - evenBegin;
     // bands: ~2.5 rounds of resident waves, whole trips (2 PD rows) per band, >= 16 rows

@@ -85,6 +85,7 @@ hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, i
 struct D32Dev {
     int srcW, srcH, dstW, dstH;
     int np;                      // producing lanes per wave (0 = auto)
+    int pd;                      // row groups loaded ahead (1, 2, 4; 0 = default 1)
     uint32_t cy[2][8];           // (c, c) u16 splats: phase p's taps at group rows 2p .. 2p + 7
     uint32_t cx[2][5];           // phase p's (c_2q, c_2q+1) int16 pairs
     uint32_t xM[2][8];           // edge-lane exact divisions (left / right 8 columns)
@@ -99,6 +100,7 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
 struct A32Dev {
     int srcW, srcH, dstW, dstH;
     int np;                      // producing lanes per wave (0 = auto)
+    int pd;                      // row pairs loaded ahead (2, 4, 8; 0 = default 4)
     uint32_t cy[2][2];           // (c, c) u16 splats of phase p's two taps
     uint32_t cx[2];              // phase p's (c_0, c_1) u16 pair
 };
