@@ -373,9 +373,10 @@ int upload_tile(iqo_hip_plan *h)
             rc = upload(&h->dWSegs, sg.data(), sg.size());
         if (rc)
             return rc;
-        iqo_amd::build_up2(h->p, h->wt, &h->ut);
-        iqo_amd::build_d32(h->p, h->wt, &h->dt);
     }
+    // exact-ratio kernels (no device tables: their coefficients are kernel arguments)
+    iqo_amd::build_up2(h->p, h->wt, &h->ut);
+    iqo_amd::build_d32(h->p, h->wt, &h->dt);
     iqo_amd::build_a32(h->p, &h->at);
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
@@ -659,9 +660,9 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_TILE;
     if (k == IQO_KERNEL_TILE && h->wt.ok && h->useWalk)
         k = IQO_KERNEL_WALK;
-    if (k == IQO_KERNEL_WALK && h->ut.ok && h->useUp2)
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->ut.ok && h->useUp2)
         k = IQO_KERNEL_LANCZOS_UP2;
-    if (k == IQO_KERNEL_WALK && h->dt.ok && h->useD32)
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->dt.ok && h->useD32)
         k = IQO_KERNEL_LANCZOS_D32;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->at.ok && h->useA32)
         k = IQO_KERNEL_AREA_D32;
@@ -687,11 +688,13 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if (kernel == IQO_KERNEL_TILE && h->wt.ok && h->useWalk && aligned(src, 4, srcSt, srcFrameSt))
         kernel = IQO_KERNEL_WALK;
     // the 2x Lanczos kernel loads 8 B per lane and stores 16 B per lane
-    if (kernel == IQO_KERNEL_WALK && h->ut.ok && h->useUp2 && aligned(src, 8, srcSt, srcFrameSt) &&
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->ut.ok && h->useUp2 &&
+        aligned(src, 8, srcSt, srcFrameSt) &&
         aligned(dst, 16, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_UP2;
     // the 3:2 Lanczos kernel loads 12 B per lane (4-byte aligned) and stores 8 B per lane
-    if (kernel == IQO_KERNEL_WALK && h->dt.ok && h->useD32 && aligned(dst, 8, dstSt, dstFrameSt))
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->dt.ok && h->useD32 &&
+        aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_D32;
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))

@@ -950,7 +950,8 @@ void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w)
 void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
 {
     *u = Up2Tables();
-    if (p.method != kLanczos || !w.ok || p.x.identity || p.y.identity || p.dstW != 2 * p.srcW ||
+    (void)w;
+    if (p.method != kLanczos || p.x.identity || p.y.identity || p.dstW != 2 * p.srcW ||
         p.dstH != 2 * p.srcH || p.dstW % 16 || p.dstW < 32 || p.dstH < 8)
         return;
     const int NT = static_cast<int>(p.x.taps);
@@ -1071,7 +1072,8 @@ void build_a32(const Plan &p, A32Tables *t)
 void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
 {
     *d = D32Tables();
-    if (p.method != kLanczos || !w.ok || p.x.identity || p.y.identity || 2 * p.srcW != 3 * p.dstW ||
+    (void)w;
+    if (p.method != kLanczos || p.x.identity || p.y.identity || 2 * p.srcW != 3 * p.dstW ||
         2 * p.srcH != 3 * p.dstH || p.dstW % 8 || p.dstW < 16 || p.dstH < 8)
         return;
     if (p.x.taps != 10 || p.y.taps != 10)

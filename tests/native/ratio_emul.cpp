@@ -1,0 +1,151 @@
+// Test-only scalar emulation of the exact-ratio kernels of kernels.hip (lanczos_d32_kernel,
+// lanczos_up2_kernel, area_d32_kernel) over the product's own tables (libiqo_amd/csrc/plan.cpp
+// build_d32 / build_up2 / build_a32), so the coordinate checks, the zero rows / columns outside
+// the image, the magic-number border divisions and the edge-lane rewrite are checked against the
+// oracle on a machine without a GPU.  Emulates the kernels' arithmetic word for word: 16-bit
+// wrapped vertical sums, v_dot2 pairs with int16 (Lanczos) or u16 (Area) halves, ydiv2, the
+// multiply-high edge division, v_ashr_pk_u8_i32 saturation.  Never part of the product.
+#include "plan.hpp"
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+using namespace iqo_amd;
+
+namespace {
+
+uint32_t umulhi(uint32_t a, uint32_t b) { return static_cast<uint32_t>((static_cast<uint64_t>(a) * b) >> 32); }
+
+// kernels.hip ydiv2 on one int16 half
+uint16_t ydiv1(uint16_t w, uint32_t m, int s)
+{
+    const int v = static_cast<int16_t>(w);
+    const uint32_t q = umulhi(static_cast<uint32_t>(v < 0 ? -v : v) << s, m);
+    return static_cast<uint16_t>(v < 0 ? 0u - q : q);
+}
+
+int sat_u8(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
+
+uint8_t edge_div(int s, uint32_t m, int t)
+{
+    const uint32_t q = umulhi(static_cast<uint32_t>(s < 0 ? 0 : s), m) >> t;
+    return static_cast<uint8_t>(q > 255u ? 255u : q);
+}
+
+}  // namespace
+
+extern "C" {
+
+// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32.  Returns 0 on success, 1 if the shape is
+// not eligible for that kernel, -1 on bad arguments.
+int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int dstW, int dstH, int pxScale,
+               const uint8_t *src, uint8_t *dst)
+{
+    Plan p;
+    std::string err;
+    if (!build_plan(static_cast<Method>(method), degree, srcW, srcH, dstW, dstH, pxScale, &p, &err))
+        return -1;
+    TileTables t;
+    WalkTables w;
+    build_tile_tables(p, &t);
+    if (t.ok)
+        build_walk_tables(p, t, &w);
+    auto px = [&](int r, int c) -> int {
+        return (r < 0 || r >= srcH || c < 0 || c >= srcW) ? 0 : src[static_cast<size_t>(r) * srcW + c];
+    };
+    std::vector<uint16_t> work(static_cast<size_t>(srcW));
+    if (kind == 0) {
+        D32Tables d;
+        build_d32(p, w, &d);
+        if (!d.ok)
+            return 1;
+        for (int y = 0; y < dstH; ++y) {
+            const int m = y >> 1, ph = y & 1;
+            for (int c = 0; c < srcW; ++c) {
+                uint16_t acc = 0;
+                for (int i = 0; i < 8; ++i)
+                    acc = static_cast<uint16_t>(acc + px(3 * m - 4 + 2 * ph + i, c) * static_cast<uint16_t>(d.cy[ph][i]));
+                if (y < d.m0 || y >= d.m1) {
+                    const int side = y < d.m0 ? 0 : 1, bi = side ? y - d.m1 : y;
+                    acc = ydiv1(acc, d.yM[side][bi], d.yS[side][bi]);
+                }
+                work[static_cast<size_t>(c)] = acc;
+            }
+            auto W = [&](int c) -> int { return (c < 0 || c >= srcW) ? 0 : static_cast<int16_t>(work[static_cast<size_t>(c)]); };
+            for (int x = 0; x < dstW; ++x) {
+                const int q = x & 1, a = 3 * (x >> 1) - 4 + q;
+                int s = 1 << 19;
+                for (int k = 0; k < 5; ++k)
+                    s += W(a + 2 * k) * static_cast<int16_t>(d.cx[q][k] & 0xffffu) +
+                         W(a + 2 * k + 1) * static_cast<int16_t>(d.cx[q][k] >> 16);
+                const int side = x < 8 ? 0 : x >= dstW - 8 ? 1 : -1;
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(
+                    side < 0 ? sat_u8(s >> 20) : edge_div(s, d.xM[side][side ? x - (dstW - 8) : x], d.xT[side][side ? x - (dstW - 8) : x]));
+            }
+        }
+        return 0;
+    }
+    if (kind == 1) {
+        Up2Tables u;
+        build_up2(p, w, &u);
+        if (!u.ok)
+            return 1;
+        const int NT = u.NT, OFF = 1 - NT / 2;
+        for (int y = 0; y < dstH; ++y) {
+            const int k = y >> 1;
+            for (int c = 0; c < srcW; ++c) {
+                uint16_t acc;
+                if ((y & 1) == 0) {
+                    acc = static_cast<uint16_t>(px(k, c) * static_cast<uint16_t>(u.cy0));
+                } else {
+                    acc = 0;
+                    for (int i = 0; i < NT; ++i)
+                        acc = static_cast<uint16_t>(acc + px(k + OFF + i, c) * static_cast<uint16_t>(u.cy1[i]));
+                }
+                if (y < u.m0 || y >= u.m1) {
+                    const int side = y < u.m0 ? 0 : 1, bi = side ? y - u.m1 : y;
+                    acc = ydiv1(acc, u.yM[side][bi], u.yS[side][bi]);
+                }
+                work[static_cast<size_t>(c)] = acc;
+            }
+            auto W = [&](int c) -> int { return (c < 0 || c >= srcW) ? 0 : static_cast<int16_t>(work[static_cast<size_t>(c)]); };
+            for (int x = 0; x < dstW; ++x) {
+                int s = 1 << 19;
+                if ((x & 1) == 0) {
+                    s += W(x >> 1) * static_cast<int16_t>(u.cx0 & 0xffffu);
+                } else {
+                    for (int q = 0; q < NT / 2; ++q)
+                        s += W((x >> 1) + OFF + 2 * q) * static_cast<int16_t>(u.cx1[q] & 0xffffu) +
+                             W((x >> 1) + OFF + 2 * q + 1) * static_cast<int16_t>(u.cx1[q] >> 16);
+                }
+                const int side = x < 16 ? 0 : x >= dstW - 16 ? 1 : -1;
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(
+                    side < 0 ? sat_u8(s >> 20) : edge_div(s, u.xM[side][side ? x - (dstW - 16) : x], u.xT[side][side ? x - (dstW - 16) : x]));
+            }
+        }
+        return 0;
+    }
+    if (kind == 2) {
+        A32Tables a;
+        build_a32(p, &a);
+        if (!a.ok)
+            return 1;
+        for (int y = 0; y < dstH; ++y) {
+            const int m = y >> 1, ph = y & 1;
+            for (int c = 0; c < srcW; ++c)
+                work[static_cast<size_t>(c)] = static_cast<uint16_t>(px(3 * m + ph, c) * static_cast<uint16_t>(a.cy[ph][0]) +
+                                                                     px(3 * m + ph + 1, c) * static_cast<uint16_t>(a.cy[ph][1]));
+            for (int x = 0; x < dstW; ++x) {
+                const int q = x & 1, s0 = 3 * (x >> 1) + q;
+                const uint32_t s = (1u << 22) + work[static_cast<size_t>(s0)] * (a.cx[q] & 0xffffu) +
+                                   work[static_cast<size_t>(s0 + 1)] * (a.cx[q] >> 16);
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(sat_u8(static_cast<int>(s) >> 23));
+            }
+        }
+        return 0;
+    }
+    return -1;
+}
+
+}  // extern "C"

@@ -51,8 +51,8 @@ def test_golden_vectors_gpu(golden, variant):
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
         if variant == "tile":
-            r.set_option("walk", 0)
-            r.set_option("a32", 0)
+            for k in ("walk", "a32", "d32", "up2"):
+                r.set_option(k, 0)
         elif variant != "default":
             r.set_option(variant, 1)
         src = ol.gen(c["gen"], sw, sh, c["seed"])
@@ -383,8 +383,8 @@ def test_tile_streamer_matches_oracle(cfg):
     frames[1, :, : sw // 3] = 255
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
     t = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    t.set_option("walk", 0)
-    t.set_option("a32", 0)
+    for k in ("walk", "a32", "d32", "up2"):
+        t.set_option(k, 0)
     assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
     for k in ("up2", "d32", "a32"):  # exact-ratio kernels off: the walker alone (their own tests below)

@@ -1,0 +1,86 @@
+"""The exact-ratio kernels' host tables (plan.cpp build_d32 / build_up2 / build_a32), run through a
+scalar emulation of the kernels' arithmetic (tests/native/ratio_emul.cpp, test-only): zero rows and
+columns outside the image, magic-number border divisions, the edge-lane rewrite.  Checked against
+the golden vectors they cover and against the oracle on random exact 3:2 and 2x shapes -- the
+CPU-side check before the GPU parity tests (tests/test_gpu_parity.py) run the kernels themselves.
+"""
+import ctypes
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+METHODS = {"lanczos": 0, "area": 1, "linear": 2}
+KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2}
+
+
+@pytest.fixture(scope="module")
+def emul():
+    out = os.path.join(HERE, "native", "_build")
+    os.makedirs(out, exist_ok=True)
+    so = os.path.join(out, "libratio_emul.so")
+    srcs = [os.path.join(HERE, "native", "ratio_emul.cpp"), os.path.join(ROOT, "libiqo_amd", "csrc", "plan.cpp")]
+    if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off",
+                               "-I" + os.path.join(ROOT, "libiqo_amd", "csrc"), "-o", so] + srcs)
+    lib = ctypes.CDLL(so)
+    lib.ratio_emul.restype = ctypes.c_int
+    lib.ratio_emul.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint] + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2
+    return lib
+
+
+def run_emul(lib, kind, method, degree, sw, sh, dw, dh, px, src):
+    dst = np.zeros((dh, dw), np.uint8)
+    src = np.ascontiguousarray(src)
+    rc = lib.ratio_emul(KINDS[kind], METHODS[method], degree, sw, sh, dw, dh, px, src.ctypes.data, dst.ctypes.data)
+    return rc, dst
+
+
+def test_ratio_tables_match_golden(emul, golden):
+    covered = 0
+    for c in golden["cases"]:
+        if c["srcW"] * c["srcH"] > 4_000_000 or c["dstW"] * c["dstH"] > 4_000_000:
+            continue
+        src = ol.gen(c["gen"], c["srcW"], c["srcH"], c["seed"])
+        for kind in KINDS:
+            rc, out = run_emul(emul, kind, c["method"], c["degree"], c["srcW"], c["srcH"], c["dstW"], c["dstH"],
+                               c["pxScale"], src)
+            assert rc in (0, 1), (c["id"], kind)
+            if rc:
+                continue
+            want = c["fnv"] if c["ofast_strict_agree"] else c["fnv_strict"]
+            assert "%016x" % ol.fnv1a64(out) == want, (c["id"], kind)
+            covered += 1
+    assert covered >= 3
+
+
+def _shapes():
+    rng = random.Random(32)
+    out = [("lanczos_d32", "lanczos", 3, 1920, 1080, 1280, 720), ("lanczos_up2", "lanczos", 3, 1920, 1080, 3840, 2160),
+           ("area_d32", "area", 0, 1920, 1080, 1280, 720), ("lanczos_up2", "lanczos", 2, 200, 60, 400, 120)]
+    for _ in range(6):
+        a, b = rng.randint(2, 40), rng.randint(4, 60)
+        out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
+        out.append(("area_d32", "area", 0, 12 * a, 3 * b, 8 * a, 2 * b))
+        out.append(("lanczos_up2", "lanczos", rng.choice((2, 3)), 8 * a, b + 4, 16 * a, 2 * b + 8))
+    return out
+
+
+@pytest.mark.parametrize("cfg", _shapes(), ids=lambda c: "%s_%dx%d" % (c[0], c[3], c[4]))
+def test_ratio_tables_match_oracle(emul, cfg):
+    kind, m, d, sw, sh, dw, dh = cfg
+    for gen, seed in (("noise", 5), ("flat255", 0), ("checker", 0)):
+        src = ol.gen(gen, sw, sh, seed)
+        rc, out = run_emul(emul, kind, m, d, sw, sh, dw, dh, 1, src)
+        if rc == 1 and min(dw, dh) < 16:
+            pytest.skip("not eligible for %s" % kind)
+        assert rc == 0, (cfg, "not eligible")
+        exp = ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)
+        bad = np.argwhere(out != exp)
+        assert bad.size == 0, (cfg, gen, bad[:4].tolist())
