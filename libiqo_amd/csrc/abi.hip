@@ -39,6 +39,7 @@ struct iqo_hip_plan {
                             // streamer, 2: per-wave symmetric streamer (all bit-identical)
     int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
+    int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
@@ -487,6 +488,7 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.dbg = h->debugFlags;
     l.prefetch = h->prefetch;
     l.ringPack = h->ringPack;
+    l.rounds = h->rounds;
     l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
     l.NX = f.NX;
     l.offXO = f.offXO;
@@ -852,6 +854,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
 #endif
+    if (!std::strcmp(key, "rounds")) {  // block-shared Lanczos streamer: auto band count (speed only)
+        if (value < -1 || value > 64)
+            return IQO_HIP_EINVAL;
+        h->rounds = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
     if (!std::strcmp(key, "ring_pack")) {  // block-shared Lanczos streamer: packed ring rows (speed only)
         h->ringPack = value != 0;
         return IQO_HIP_OK;

@@ -3067,8 +3067,20 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
                : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 2>)
                          : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 3>);
     }
-    if (bands <= 0)
-        bands = choose_bands(rows, io.frames, wpr, resident_waves(kern, block, ldsBytes), l.NY - 2);
+    if (bands <= 0) {
+        const int resident = resident_waves(kern, block, ldsBytes);
+        if (shared && l.rounds >= 0) {
+            // block-shared ring: about `rounds` rounds of resident workgroups (default 6), bands of
+            // >= 16 rows.  On fresh data more, shorter bands beat the one-round makespan optimum
+            // (C2 x128: 8 bands 0.305 ms, 24 0.296, 48 0.294): workgroups that start and finish at
+            // different times spread their requests over the memory channels, and the halo rows of
+            // neighbouring bands (same XCD) come from L2
+            const int64_t want = static_cast<int64_t>(l.rounds > 0 ? l.rounds : 6) * (resident / wpr);
+            bands = static_cast<int>(std::min<int64_t>((want + io.frames - 1) / io.frames, std::max(1, rows / 16)));
+        } else {
+            bands = choose_bands(rows, io.frames, wpr, resident, l.NY - 2);
+        }
+    }
     bands = max(1, min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
