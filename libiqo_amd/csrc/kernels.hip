@@ -2954,11 +2954,13 @@ hipError_t launch_a32(const A32Dev &d, const Io &io, int rowBegin, int rowEnd, i
                                    : reinterpret_cast<const void *>(area_d32_kernel<4>);
     const int evenBegin = rowBegin & ~1;
     const int rows = rowEnd - evenBegin;
-    // bands: ~2.5 rounds of resident waves, whole trips (2 PD rows) per band, >= 16 rows
+    // bands: ~6 rounds of resident waves, whole trips (8 rows) per band (fresh data, G3: 90 bands
+    // of 8 rows 0.0712 ms vs 0.0742 at ~2.5 rounds; the kernel has no window, so short bands
+    // cost nothing)
     if (bands <= 0) {
         const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
         const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
-        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
+        bands = static_cast<int>(std::min<int64_t>((6 * resident + perBand - 1) / perBand, std::max(1, rows / 8)));
     }
     bands = std::max(1, std::min(bands, (rows + 7) / 8));
     int rpb = (rows + bands - 1) / bands;
@@ -3164,8 +3166,12 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
                                        : reinterpret_cast<const void *>(linear_up2_kernel<4, false>))
                                  : (nt ? reinterpret_cast<const void *>(linear_up2_kernel<2, true>)
                                        : reinterpret_cast<const void *>(linear_up2_kernel<2, false>));
-    if (bands <= 0)
-        bands = choose_bands(rows, io.frames, wpr, resident_waves(kern), 2);
+    if (bands <= 0) {
+        // ~6 rounds of resident waves, >= 16 rows per band (fresh data, C4 x256: 48 bands 0.537 ms
+        // vs 0.555 for the one-round makespan choice)
+        const int64_t want = 6 * static_cast<int64_t>(resident_waves(kern)) / wpr;
+        bands = static_cast<int>(std::min<int64_t>((want + io.frames - 1) / io.frames, std::max(1, rows / 16)));
+    }
     bands = max(1, min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
