@@ -47,10 +47,22 @@ __device__ __forceinline__ unsigned xcd_spread(unsigned L, unsigned n)
     return xcd < r ? xcd * (q + 1u) + idx : r * (q + 1u) + (xcd - r) * q + idx;
 }
 
-// 16-byte streaming load (source pixels are read once per band): nontemporal hint.
+#ifndef IQO_LIN_LOAD_NT
+#define IQO_LIN_LOAD_NT 1  // Linear 2x streamer: nontemporal source loads
+#endif
+
+// 16-byte streaming load (source pixels are read once per band): nontemporal hint unless
+// IQO_AREA_LOAD_NT = 0.
+#ifndef IQO_AREA_LOAD_NT
+#define IQO_AREA_LOAD_NT 1
+#endif
 __device__ __forceinline__ uint4 load16_nt(const uint8_t *p)
 {
+#if IQO_AREA_LOAD_NT
     u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+#else
+    u32x4 v = *reinterpret_cast<const u32x4 *>(p);
+#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -801,7 +813,8 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 // 16-byte-per-lane LDS-DMA of one source row into LDS bytes [lds, lds + 1024) of this wave.
 // M0 is saved and restored inside the statement (it is compiler-reserved).
 #ifndef IQO_DMA_NT
-#define IQO_DMA_NT 1  // nontemporal LDS-DMA source reads (each source row is read once)
+#define IQO_DMA_NT 0  // LDS-DMA source reads with the default cache policy (fresh data, C2: 2.7 % faster than
+                     // nontemporal: the halo rows neighbouring bands share stay in L2)
 #endif
 __device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff, bool nt = IQO_DMA_NT)
 {
@@ -827,11 +840,19 @@ __device__ __forceinline__ void dma_row_masked(uint32_t lds, int voff, __amdgpu_
 {
     uint32_t keep;
     uint64_t save;
+#if IQO_DMA_NT
     asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                  "buffer_load_dwordx4 %3, %4, %5 offen nt lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
                  : "=&s"(keep), "=&s"(save)
                  : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
                  : "memory");
+#else
+    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %4, %5 offen lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+                 : "=&s"(keep), "=&s"(save)
+                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
+                 : "memory");
+#endif
 }
 
 template <int N>
@@ -1911,7 +1932,7 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
 
     auto load_row = [&](int r) -> u32x2 {
         return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff, r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000,
-                                                    2 /* nt */);
+                                                    IQO_LIN_LOAD_NT ? 2 /* nt */ : 0);
     };
     auto unpack = [&](u32x2 v, uint32_t (&P)[5]) {
         const uint32_t left = static_cast<uint32_t>(
