@@ -48,7 +48,8 @@ __device__ __forceinline__ unsigned xcd_spread(unsigned L, unsigned n)
 }
 
 #ifndef IQO_LIN_LOAD_NT
-#define IQO_LIN_LOAD_NT 1  // Linear 2x streamer: nontemporal source loads
+#define IQO_LIN_LOAD_NT 0  // Linear 2x streamer: default-policy source loads (fresh data C4: 1 % faster
+                           // than nontemporal; the Area streamer keeps nontemporal: 9 % faster on C3)
 #endif
 
 // 16-byte streaming load (source pixels are read once per band): nontemporal hint unless
