@@ -1114,6 +1114,9 @@ template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
 #ifndef IQO_SYMB_LA
 #define IQO_SYMB_LA 1  // LDS look-ahead in the block-shared streamer (C2: ~1% faster)
 #endif
+#ifndef IQO_SYMB_NT_STORE
+#define IQO_SYMB_NT_STORE 0
+#endif
 #ifndef IQO_SYMB_EDGE_BATCH
 #define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (C2: 64 -> 16 cuts write traffic +4.5% -> +2%)
 #endif
@@ -1426,7 +1429,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{o.x, o.y, o.x, o.y}, dstR, st16, (yy - a.io.dstRow0) * dstSt, 0);
         } else
 #endif
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, IQO_SYMB_NT_STORE ? 2 : 0);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every 64 rows and at the band end one pass divides them, one row per lane
@@ -2063,6 +2066,15 @@ struct Up2Args {
     unsigned nWaves;
 };
 
+#ifndef IQO_UP2_NT_STORE
+#define IQO_UP2_NT_STORE 1  // nontemporal 16-B stores (fresh data G2: 0.088 vs 0.1015 ms)
+#endif
+#ifndef IQO_D32_NT_STORE
+#define IQO_D32_NT_STORE 0
+#endif
+#ifndef IQO_A32_NT_STORE
+#define IQO_A32_NT_STORE 0
+#endif
 template <int NT>
 __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
 {
@@ -2123,7 +2135,8 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
         P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);  // (cb+6, cb+7)
     };
     auto store_row = [&](u32x4 o, int voffs, int y, bool ok) {
-        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0,
+                                               IQO_UP2_NT_STORE ? 2 /* nt */ : 0);
     };
     // masked border row (uniform, rare): work = int16(n * 64 / deno)
     auto border_row = [&](uint32_t (&W)[4], int y) {
@@ -2360,7 +2373,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         P[5] = __builtin_amdgcn_perm(0u, v.z, 0x0c030c02u);  // (cb+10, cb+11)
     };
     auto store_row = [&](u32x2 o, int voffs, int y, bool ok) {
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, IQO_D32_NT_STORE ? 2 : 0);
     };
     // horizontal pass of one output row from the lane's six work pairs; the edge lane parks its sums
     auto emit = [&](const uint32_t (&W)[6], int y, int slot) {
@@ -2573,7 +2586,7 @@ __global__ __launch_bounds__(256) void area_d32_kernel(A32Args a)
                         udot2(E[2], d.cx[1], b));
         o.y = pack23_hi(pack23_lo(udot2(E[3], d.cx[0], b), udot2(O7, d.cx[1], b)), udot2(O9, d.cx[0], b),
                         udot2(E[5], d.cx[1], b));
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff + (y >= y0 && y < y1 ? (y - dstRow0) * dstSt : OOB), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff + (y >= y0 && y < y1 ? (y - dstRow0) * dstSt : OOB), 0, IQO_A32_NT_STORE ? 2 : 0);
     };
 
     u32x3 pre[PD][3];
