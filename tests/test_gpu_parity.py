@@ -491,7 +491,9 @@ YUV_CASES = [
     ("lanczos", 2, 640, 480, 320, 240, True),       # per-wave symmetric Y (1 wave per row) + ring chroma
     ("area", 0, 7680, 4320, 1920, 1080, True),
     ("linear", 0, 1920, 1080, 3840, 2160, True),
-    ("lanczos", 3, 1920, 1080, 1280, 720, False),   # general kernel: plane by plane
+    ("lanczos", 3, 1920, 1080, 1280, 720, False),   # plane by plane: exact 3:2 kernel on Y
+    ("lanczos", 3, 960, 540, 1920, 1080, False),     # plane by plane: exact 2x kernel on Y
+    ("area", 0, 1920, 1080, 1280, 720, False),       # plane by plane: exact 3:2 Area kernel
 ]
 
 
