@@ -813,6 +813,9 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 
 // 16-byte-per-lane LDS-DMA of one source row into LDS bytes [lds, lds + 1024) of this wave.
 // M0 is saved and restored inside the statement (it is compiler-reserved).
+#ifndef IQO_SYMB_PRO_NT
+#define IQO_SYMB_PRO_NT 0  // window prologue loads: default policy (the neighbouring band reads the same halo rows)
+#endif
 #ifndef IQO_DMA_NT
 #define IQO_DMA_NT 0  // LDS-DMA source reads with the default cache policy (fresh data, C2: 2.7 % faster than
                      // nontemporal: the halo rows neighbouring bands share stay in L2)
@@ -983,7 +986,7 @@ __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, co
         uint4 w0[NY - 2];
 #pragma unroll
         for (int t = 0; t < NY - 2; ++t) {
-            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), 2 /* nt */);
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), IQO_SYMB_PRO_NT ? 2 : 0);
             w0[t] = make_uint4(q.x, q.y, q.z, q.w);
         }
 #pragma unroll
@@ -1274,7 +1277,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         uint4 w0[NY - 2];
 #pragma unroll
         for (int t = 0; t < NY - 2; ++t) {
-            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), 2 /* nt */);
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), IQO_SYMB_PRO_NT ? 2 : 0);
             w0[t] = make_uint4(q.x, q.y, q.z, q.w);
         }
 #pragma unroll
