@@ -35,8 +35,8 @@ fi
 if want pmc; then
   cd /tmp || exit 1
   for c in ${PMC_CFGS:-c2 c3 c4 g1}; do
-    timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify > "$OUT/pmc_fetch_$c.log" 2>&1 || { echo "pmc fetch $c failed"; tail -20 "$OUT/pmc_fetch_$c.log"; exit 1; }
-    timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify > "$OUT/pmc_write_$c.log" 2>&1 || { echo "pmc write $c failed"; tail -20 "$OUT/pmc_write_$c.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify --no-probe > "$OUT/pmc_fetch_$c.log" 2>&1 || { echo "pmc fetch $c failed"; tail -20 "$OUT/pmc_fetch_$c.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify --no-probe > "$OUT/pmc_write_$c.log" 2>&1 || { echo "pmc write $c failed"; tail -20 "$OUT/pmc_write_$c.log"; exit 1; }
   done
   cd "$ROOT" || exit 1
 fi
