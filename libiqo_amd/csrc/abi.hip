@@ -609,6 +609,7 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     d.dstH = h->p.dstH;
     d.np = h->lanes;
     d.pd = h->ratioPrefetch;
+    d.variant = t.variant;
     std::memcpy(d.cy, t.cy, sizeof d.cy);
     std::memcpy(d.cx, t.cx, sizeof d.cx);
     std::memcpy(d.xM, t.xM, sizeof d.xM);

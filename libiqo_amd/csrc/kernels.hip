@@ -2312,11 +2312,17 @@ struct D32Args {
     unsigned nWaves;
 };
 
-template <int PD>
+// Tap structure (plan.cpp build_d32): group m's window is source rows 3m + GA .. 3m + GA + GW - 1;
+// the even row's NTY taps start at group row 0, the odd row's at group row PO1; output column x
+// takes NPX coefficient pairs from column 3 (x >> 1) + BX0 + (x & 1).  Lanczos-3: <-4, 10, 8, 2,
+// 5, -4>; Lanczos-2: <-2, 7, 5, 2, 3, -2>.
+template <int PD, int GA, int GW, int NTY, int PO1, int NPX, int BX0>
 __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
 {
-    constexpr int NW = 12;     // register window rows: a group's 10 + the 2 the next group adds early
-    constexpr int U = NW / 3;  // groups per unrolled trip (window slots repeat)
+    constexpr int NW = (GW + 2) / 3 * 3;  // register window rows (a multiple of the 3 rows a group adds)
+    constexpr int U = NW / 3;             // groups per unrolled trip (window slots repeat)
+    static_assert(GW >= 3 && NTY <= 8 && NPX <= 5 && PO1 + NTY <= GW, "tap structure");
+    static_assert(BX0 >= -4 && 9 + BX0 + 1 + 2 * NPX - 1 <= 15, "column windows within the lane's work pairs");
     constexpr int OOB = 0x7ff00000;
     static_assert(U % PD == 0, "prefetch slots repeat within a trip");
     const D32Dev &d = a.d;
@@ -2358,8 +2364,8 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     // border sums); rows of dropped outputs may lie outside the call's window: clamped (their
     // values are never used); rows past the band's last group are not loaded.  Out-of-range marks
     // go in the (range-checked) VGPR offset.
-    const int rBase = 3 * kLo - 4;
-    const int rLast = 3 * (kLo + nG - 1) + 5;
+    const int rBase = 3 * kLo + GA;
+    const int rLast = 3 * (kLo + nG - 1) + GA + GW - 1;
     const int srcLast = a.io.srcRowEnd - 1;
     auto load_row = [&](int q) -> u32x3 {
         const int r = rBase + q;
@@ -2397,10 +2403,10 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int ph = j & 1;
-            const int rel = 3 * (j >> 1) - 4 + ph;  // window start of output x0 + 8(l-1) + j
+            const int rel = 3 * (j >> 1) + BX0 + ph;  // window start of output x0 + 8(l-1) + j
             int acc = sdot2(pair(rel), d.cx[ph][0], 1 << 19);
 #pragma unroll
-            for (int q = 1; q < 5; ++q)
+            for (int q = 1; q < NPX; ++q)
                 acc = sdot2(pair(rel + 2 * q), d.cx[ph][q], acc);
             sum[j] = acc;
         }
@@ -2416,7 +2422,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
             }
         }
     };
-    // once per trip: lane r < 8 rewrites the edge bytes of row yt + r from the parked sums
+    // once per trip: lane r < 2U rewrites the edge bytes of row yt + r from the parked sums
     auto flush = [&](int yt) {
         u32x2 oL = {0u, 0u}, oR = {0u, 0u};
         if (edgeL || edgeR) {  // uniform
@@ -2436,7 +2442,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
                 oR = fix(1);
         }
         const int y = yt + lane;
-        const bool ok = lane < 8 && y >= y0 && y < y1;
+        const bool ok = lane < 2 * U && y >= y0 && y < y1;
         store_row(oL, edgeL ? 0 : OOB, y, ok);
         store_row(oR, edgeR ? d.dstW - 8 : OOB, y, ok);
     };
@@ -2454,18 +2460,18 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     };
 
     uint32_t R[NW][6];
-    // the window of group 0 without the rows group 0 itself adds: relative rows 0..6 -> slots 0..6
+    // the window of group 0 without the rows group 0 itself adds: relative rows 0 .. GW-4 -> slots
 #pragma unroll
-    for (int q = 0; q < 7; ++q)
+    for (int q = 0; q < GW - 3; ++q)
         widen(load_row(q), R[q]);
-    // prefetch: group g adds relative rows 3g + 7 .. 3g + 9 (slots (3g + 7 .. 3g + 9) % NW)
+    // prefetch: group g adds relative rows 3g + GW - 3 .. 3g + GW - 1 (slots mod NW)
     u32x3 pre[PD][3];
 #pragma unroll
     for (int v = 0; v < PD; ++v) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 3; ++i)
-            pre[v][i] = load_row(3 * v + 7 + i);
+            pre[v][i] = load_row(3 * v + GW - 3 + i);
         // the loop's store pattern (two rows per group), dropped, so the header waits are steady-state
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, OOB, 0, 0);
@@ -2480,17 +2486,17 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
-                widen(pre[v % PD][i], R[(3 * v + 7 + i) % NW]);
+                widen(pre[v % PD][i], R[(3 * v + GW - 3 + i) % NW]);
 #pragma unroll
             for (int i = 0; i < 3; ++i)
-                pre[v % PD][i] = load_row(3 * (g + PD) + 7 + i);
+                pre[v % PD][i] = load_row(3 * (g + PD) + GW - 3 + i);
             const int y = 2 * (kLo + g);
             uint32_t W[6];
 #pragma unroll
             for (int c = 0; c < 6; ++c)
                 W[c] = pk_mul(R[(3 * v) % NW][c], d.cy[0][0]);
 #pragma unroll
-            for (int t = 1; t < 8; ++t)
+            for (int t = 1; t < NTY; ++t)
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
                     W[c] = pk_mad(R[(3 * v + t) % NW][c], d.cy[0][t], W[c]);
@@ -2498,12 +2504,12 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
             emit(W, y, 2 * v);
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-                W[c] = pk_mul(R[(3 * v + 2) % NW][c], d.cy[1][0]);
+                W[c] = pk_mul(R[(3 * v + PO1) % NW][c], d.cy[1][0]);
 #pragma unroll
-            for (int t = 1; t < 8; ++t)
+            for (int t = 1; t < NTY; ++t)
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
-                    W[c] = pk_mad(R[(3 * v + 2 + t) % NW][c], d.cy[1][t], W[c]);
+                    W[c] = pk_mad(R[(3 * v + PO1 + t) % NW][c], d.cy[1][t], W[c]);
             border_row(W, y + 1);
             emit(W, y + 1, 2 * v + 1);
         });
@@ -2949,9 +2955,16 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     int np = d.np > 0 ? min(d.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
     // one group of rows loaded ahead by default (G1, fresh data: 2.5 % faster than 2, 8 % than 4)
-    const void *kern = d.pd == 2   ? reinterpret_cast<const void *>(lanczos_d32_kernel<2>)
-                       : d.pd == 4 ? reinterpret_cast<const void *>(lanczos_d32_kernel<4>)
-                                   : reinterpret_cast<const void *>(lanczos_d32_kernel<1>);
+    const void *kern = nullptr;
+    if (d.variant == 0)
+        kern = d.pd == 2   ? reinterpret_cast<const void *>(lanczos_d32_kernel<2, -4, 10, 8, 2, 5, -4>)
+               : d.pd == 4 ? reinterpret_cast<const void *>(lanczos_d32_kernel<4, -4, 10, 8, 2, 5, -4>)
+                           : reinterpret_cast<const void *>(lanczos_d32_kernel<1, -4, 10, 8, 2, 5, -4>);
+    else if (d.variant == 1)
+        kern = d.pd == 3 ? reinterpret_cast<const void *>(lanczos_d32_kernel<3, -2, 7, 5, 2, 3, -2>)
+                         : reinterpret_cast<const void *>(lanczos_d32_kernel<1, -2, 7, 5, 2, 3, -2>);
+    else
+        return hipErrorInvalidValue;
     const int evenBegin = rowBegin & ~1;
     const int rows = rowEnd - evenBegin;
     // bands: ~2.5 rounds of resident waves, whole trips (8 rows) per band, >= 16 rows
@@ -2960,9 +2973,10 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
         const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
         bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
     }
-    bands = std::max(1, std::min(bands, (rows + 7) / 8));
+    const int trip = d.variant == 0 ? 8 : 6;  // output rows per unrolled trip (2 U)
+    bands = std::max(1, std::min(bands, (rows + trip - 1) / trip));
     int rpb = (rows + bands - 1) / bands;
-    rpb = (rpb + 7) & ~7;
+    rpb = (rpb + trip - 1) / trip * trip;
     bands = (rows + rpb - 1) / rpb;
     const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
     if (nWaves >= (uint64_t(1) << 31))

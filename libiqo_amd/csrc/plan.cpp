@@ -1076,9 +1076,24 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
     if (p.method != kLanczos || p.x.identity || p.y.identity || 2 * p.srcW != 3 * p.dstW ||
         2 * p.srcH != 3 * p.dstH || p.dstW % 8 || p.dstW < 16 || p.dstH < 8)
         return;
-    if (p.x.taps != 10 || p.y.taps != 10)
+    // the instantiated tap structures (kernels.hip lanczos_d32_kernel): taps T, group window start
+    // GA (= the even rows' window start relative to 3m) and length GW, taps per row NTY, the odd
+    // rows' first group row PO1, coefficient pairs per column NPX, column window start BX0
+    struct Shape {
+        int T, GA, GW, NTY, PO1, NPX, BX0;
+    };
+    static const Shape kShapes[2] = {{10, -4, 10, 8, 2, 5, -4}, {6, -2, 7, 5, 2, 3, -2}};
+    const int T = static_cast<int>(p.x.taps);
+    if (static_cast<int>(p.y.taps) != T)
         return;
-    auto start_ok = [](const Window &win, int i) { return win.start == 3 * (i >> 1) - 4 + (i & 1); };
+    int vi = -1;
+    for (int k = 0; k < 2; ++k)
+        if (kShapes[k].T == T)
+            vi = k;
+    if (vi < 0)
+        return;
+    const Shape &S = kShapes[vi];
+    auto start_ok = [](const Window &win, int i, int b0) { return win.start == 3 * (i >> 1) + b0 + (i & 1); };
     auto phase_row = [](const AxisPlan &ax, int ph) {
         return std::vector<int32_t>(ax.table.begin() + ph * ax.taps, ax.table.begin() + (ph + 1) * ax.taps);
     };
@@ -1089,7 +1104,7 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
     for (int x = 0; x < p.dstW; ++x) {
         const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
         const Window win = axis_window(p, p.x, x, true);
-        if (!start_ok(win, x) || ci.tabOff % p.x.taps != 0)
+        if (!start_ok(win, x, S.BX0) || ci.tabOff % p.x.taps != 0)
             return;
         const std::vector<int32_t> c = phase_row(p.x, ci.tabOff / p.x.taps);
         std::vector<int32_t> &ref = xs[x & 1];
@@ -1113,7 +1128,7 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
     for (int y = 0; y < p.dstH; ++y) {
         const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
         const Window win = axis_window(p, p.y, y, false);
-        if (!start_ok(win, y) || ci.tabOff % p.y.taps != 0)
+        if (!start_ok(win, y, S.GA) || ci.tabOff % p.y.taps != 0)
             return;
         std::vector<int32_t> &ref = ys[y & 1];
         const std::vector<int32_t> c = phase_row(p.y, ci.tabOff / p.y.taps);
@@ -1122,7 +1137,7 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
         if (ref != c)
             return;
         if (!win.border) {
-            if (win.start < 0 || win.start + 10 > p.srcH)
+            if (win.start < 0 || win.start + T > p.srcH)
                 return;
             if (m0 < 0)
                 m0 = y;
@@ -1147,20 +1162,24 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
             return;
     }
     // group rows: the even row's tap t is group row t, the odd row's tap t group row t + 1; the
-    // kernel multiplies group rows 0..7 (even) and 2..9 (odd)
-    for (int t = 0; t < 10; ++t) {
-        if ((t >= 8 && ys[0][static_cast<size_t>(t)] != 0) || ((t < 1 || t > 8) && ys[1][static_cast<size_t>(t)] != 0))
+    // kernel multiplies group rows 0 .. NTY-1 (even) and PO1 .. PO1+NTY-1 (odd)
+    for (int t = 0; t < T; ++t) {
+        if ((t >= S.NTY && ys[0][static_cast<size_t>(t)] != 0) ||
+            ((t + 1 < S.PO1 || t + 1 >= S.PO1 + S.NTY) && ys[1][static_cast<size_t>(t)] != 0))
             return;
     }
     auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
-    for (int t = 0; t < 8; ++t) {
-        d->cy[0][t] = splat(ys[0][static_cast<size_t>(t)]);
-        d->cy[1][t] = splat(ys[1][static_cast<size_t>(t + 1)]);
+    for (int t = 0; t < S.NTY; ++t) {
+        d->cy[0][t] = splat(t < T ? ys[0][static_cast<size_t>(t)] : 0);
+        const int u = S.PO1 - 1 + t;
+        d->cy[1][t] = splat(u >= 0 && u < T ? ys[1][static_cast<size_t>(u)] : 0);
     }
+    auto tap = [&](int ph, int k) { return k < T ? xs[ph][static_cast<size_t>(k)] : 0; };
     for (int ph = 0; ph < 2; ++ph)
-        for (int q = 0; q < 5; ++q)
-            d->cx[ph][q] = (static_cast<uint32_t>(xs[ph][static_cast<size_t>(2 * q)]) & 0xffffu) |
-                           (static_cast<uint32_t>(xs[ph][static_cast<size_t>(2 * q + 1)]) << 16);
+        for (int q = 0; q < S.NPX; ++q)
+            d->cx[ph][q] = (static_cast<uint32_t>(tap(ph, 2 * q)) & 0xffffu) |
+                           (static_cast<uint32_t>(tap(ph, 2 * q + 1)) << 16);
+    d->variant = vi;
     d->m0 = m0;
     d->m1 = m1;
     d->ok = true;

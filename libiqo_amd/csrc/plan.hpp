@@ -205,15 +205,17 @@ struct Up2Tables {
 };
 void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u);
 
-// Exact 3:2 Lanczos-3 downscale (kernels.hip lanczos_d32_kernel), e.g. 1920x1080 -> 1280x720.  In
-// the reference's tables for this ratio output y (x) takes the 10 taps of phase y & 1 starting at
-// 3 * (y >> 1) - 4 + (y & 1).  Output rows come in groups m (rows 2m, 2m+1) over the 10 source rows
-// 3m - 4 .. 3m + 5: the even row's non-zero taps are group rows 0..7, the odd row's 2..9.  The kernel
+// Exact 3:2 Lanczos-2/3 downscale (kernels.hip lanczos_d32_kernel), e.g. 1920x1080 -> 1280x720.  In
+// the reference's tables for this ratio output y (x) takes the taps of phase y & 1 starting at
+// 3 * (y >> 1) + B + (y & 1) (Lanczos-3: 10 taps, B = -4; Lanczos-2: 6 taps, B = -2).  Output rows
+// come in groups m (rows 2m, 2m+1) over the source rows 3m + B .. (Lanczos-3: 10 rows, the even
+// row's non-zero taps group rows 0..7, the odd row's 2..9; Lanczos-2: 7 rows, 0..4 and 2..6).  The kernel
 // takes every row and column: source rows / columns outside the image read as zero, so the masked
 // border numerators come out of the same sums, and the <= 8 border rows / columns per side are
 // divided in the kernel.
 struct D32Tables {
     bool ok = false;
+    int variant = 0;                // tap structure: 0 Lanczos-3 (10 taps), 1 Lanczos-2 (6 taps)
     int m0 = 0, m1 = 0;             // main rows; rows y < m0 and y >= m1 are masked border rows
     uint32_t yM[2][8] = {};         // border row y (top: y, bottom: y - m1): int16(n * 64 / deno)
     int32_t yS[2][8] = {};          //   by magic_y

@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Kernel time and HBM roofline fraction over common video scaling ratios, on fresh device batches
+(distinct batches cycled, >= 2.5 GB per cycle, as bench.py), each output checked against the oracle
+on one frame.  Output: one line per shape (profiles/r02/ratio_sweep.txt).
+
+  python scripts/ratio_sweep.py [--steps 20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+SHAPES = [
+    # method, degree, srcW, srcH, dstW, dstH
+    ("lanczos", 3, 3840, 2160, 2560, 1440),
+    ("lanczos", 3, 3840, 2160, 1920, 1080),
+    ("lanczos", 3, 3840, 2160, 1280, 720),
+    ("lanczos", 3, 1920, 1080, 1280, 720),
+    ("lanczos", 3, 1920, 1080, 960, 540),
+    ("lanczos", 3, 1920, 1080, 854, 480),
+    ("lanczos", 3, 1280, 720, 1920, 1080),
+    ("lanczos", 3, 1920, 1080, 3840, 2160),
+    ("lanczos", 2, 1920, 1080, 1280, 720),
+    ("lanczos", 2, 1920, 1080, 960, 540),
+    ("area", 0, 3840, 2160, 1920, 1080),
+    ("area", 0, 1920, 1080, 1280, 720),
+    ("area", 0, 1920, 1080, 854, 480),
+    ("linear", 0, 1920, 1080, 3840, 2160),
+    ("linear", 0, 1280, 720, 1920, 1080),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    import libiqo_amd
+    import oracle_lib as ol
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev)
+    print("%-8s %-3s %-11s %-11s %-14s %9s %8s %7s %s" % ("method", "deg", "src", "dst", "kernel", "frames", "ms", "%peak", "parity"))
+    for m, d, sw, sh, dw, dh in SHAPES:
+        per = sw * sh + dw * dh
+        frames = max(8, min(256, int(1.3e9 // per)))
+        rot = max(2, int(-(-2.5e9 // (per * frames))))
+        r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh)
+        kern = r.describe()["kernel"]
+        src = torch.randint(0, 256, (rot, frames, sh, sw), dtype=torch.uint8, device=dev)
+        dst = torch.empty((rot, frames, dh, dw), dtype=torch.uint8, device=dev)
+
+        def launch(b):
+            r.resize_device(frames, sw, sw * sh, src[b].data_ptr(), dw, dw * dh, dst[b].data_ptr(), s.cuda_stream)
+
+        for i in range(2 * rot):
+            launch(i % rot)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for i in range(args.steps):
+            launch(i % rot)
+        e1.record(s)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / args.steps
+        exp = ol.run_oracle(m, d, sw, sh, dw, dh, 1, src[0, 0].cpu().numpy())
+        ok = bool((dst[0, 0].cpu().numpy() == exp).all())
+        frac = per * frames / (ms * 1e-3) / 8e12
+        print("%-8s %-3d %-11s %-11s %-14s %9d %8.4f %6.1f%% %s" % (m, d, "%dx%d" % (sw, sh), "%dx%d" % (dw, dh), kern,
+                                                                  frames, ms, 100 * frac, "bit-exact" if ok else "MISMATCH"),
+              flush=True)
+        del src, dst
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

@@ -60,12 +60,15 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
         build_d32(p, w, &d);
         if (!d.ok)
             return 1;
+        // the kernel instantiation's tap structure (kernels.hip launch_d32): GA, NTY, PO1, NPX, BX0
+        const int GA = d.variant ? -2 : -4, NTY = d.variant ? 5 : 8, PO1 = 2, NPX = d.variant ? 3 : 5;
+        const int BX0 = d.variant ? -2 : -4;
         for (int y = 0; y < dstH; ++y) {
             const int m = y >> 1, ph = y & 1;
             for (int c = 0; c < srcW; ++c) {
                 uint16_t acc = 0;
-                for (int i = 0; i < 8; ++i)
-                    acc = static_cast<uint16_t>(acc + px(3 * m - 4 + 2 * ph + i, c) * static_cast<uint16_t>(d.cy[ph][i]));
+                for (int i = 0; i < NTY; ++i)
+                    acc = static_cast<uint16_t>(acc + px(3 * m + GA + (ph ? PO1 : 0) + i, c) * static_cast<uint16_t>(d.cy[ph][i]));
                 if (y < d.m0 || y >= d.m1) {
                     const int side = y < d.m0 ? 0 : 1, bi = side ? y - d.m1 : y;
                     acc = ydiv1(acc, d.yM[side][bi], d.yS[side][bi]);
@@ -74,9 +77,9 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
             }
             auto W = [&](int c) -> int { return (c < 0 || c >= srcW) ? 0 : static_cast<int16_t>(work[static_cast<size_t>(c)]); };
             for (int x = 0; x < dstW; ++x) {
-                const int q = x & 1, a = 3 * (x >> 1) - 4 + q;
+                const int q = x & 1, a = 3 * (x >> 1) + BX0 + q;
                 int s = 1 << 19;
-                for (int k = 0; k < 5; ++k)
+                for (int k = 0; k < NPX; ++k)
                     s += W(a + 2 * k) * static_cast<int16_t>(d.cx[q][k] & 0xffffu) +
                          W(a + 2 * k + 1) * static_cast<int16_t>(d.cx[q][k] >> 16);
                 const int side = x < 8 ? 0 : x >= dstW - 8 ? 1 : -1;

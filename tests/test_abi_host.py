@@ -102,7 +102,8 @@ def test_host_tables_match_oracle_random():
     (("linear", 0, 1920, 1080, 3840, 2160, 1), "linear_up2"),
     (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "lanczos_up2"),   # exact 2x Lanczos: register-window streamer
     (("lanczos", 3, 1921, 1080, 3842, 2160, 1), "walk"),          # general ratios: wave walker
-    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "walk"),
+    (("lanczos", 2, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-2
+    (("lanczos", 4, 1920, 1080, 1280, 720, 1), "walk"),
     (("area", 0, 1920, 1080, 1280, 720, 1), "area_d32"),          # exact 3:2 Area: no window, no halo
     (("lanczos", 3, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-3: register window
     (("area", 0, 1921, 1080, 1280, 720, 1), "walk"),
