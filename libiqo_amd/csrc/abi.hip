@@ -62,6 +62,9 @@ struct iqo_hip_plan {
     // exact 3:2 Lanczos-3 downscale kernel on the main rows (option "d32" = 0: walker only)
     iqo_amd::D32Tables dt;
     bool useD32 = true;
+    // exact 2:3 Lanczos-3 upscale kernel (option "u23" = 0: walker only)
+    iqo_amd::U23Tables vt;
+    bool useU23 = true;
     // exact 3:2 Area downscale kernel (option "a32" = 0: walker only)
     iqo_amd::A32Tables at;
     bool useA32 = true;
@@ -379,6 +382,7 @@ int upload_tile(iqo_hip_plan *h)
     iqo_amd::build_up2(h->p, h->wt, &h->ut);
     iqo_amd::build_d32(h->p, h->wt, &h->dt);
     iqo_amd::build_a32(h->p, &h->at);
+    iqo_amd::build_u23(h->p, &h->vt);
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
     for (size_t y = 0; y < t.rows.size(); ++y)
@@ -621,6 +625,29 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::U23Dev u23_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::U23Tables &t = h->vt;
+    iqo_amd::U23Dev d;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.np = h->lanes;
+    d.pd = h->ratioPrefetch;
+    d.cy0 = t.cy0;
+    d.cx0 = t.cx0;
+    std::memcpy(d.cy, t.cy, sizeof d.cy);
+    std::memcpy(d.cx, t.cx, sizeof d.cx);
+    std::memcpy(d.xM, t.xM, sizeof d.xM);
+    std::memcpy(d.xT, t.xT, sizeof d.xT);
+    d.m0 = t.m0;
+    d.m1 = t.m1;
+    std::memcpy(d.yM, t.yM, sizeof d.yM);
+    std::memcpy(d.yS, t.yS, sizeof d.yS);
+    return d;
+}
+
 iqo_amd::A32Dev a32_dev(const iqo_hip_plan *h)
 {
     iqo_amd::A32Dev d;
@@ -669,6 +696,8 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_LANCZOS_D32;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->at.ok && h->useA32)
         k = IQO_KERNEL_AREA_D32;
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->vt.ok && h->useU23)
+        k = IQO_KERNEL_LANCZOS_U23;
     return k;
 }
 
@@ -702,6 +731,10 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_AREA_D32;
+    // the 2:3 Lanczos kernel loads 8 B per lane and stores 12 B per lane
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->vt.ok && h->useU23 &&
+        aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_LANCZOS_U23;
     return kernel;
 }
 
@@ -775,6 +808,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_d32(d32_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_AREA_D32)
             e = iqo_amd::launch_a32(a32_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_LANCZOS_U23)
+            e = iqo_amd::launch_u23(u23_dev(h), io, rb, re, h->bands, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -912,6 +947,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "up2")) {  // 0: exact 2x Lanczos upscales use the wave walker alone
         h->useUp2 = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "u23")) {  // 0: exact 2:3 Lanczos-3 upscales use the wave walker alone
+        h->useU23 = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "a32")) {  // 0: exact 3:2 Area downscales use the wave walker alone
@@ -1436,6 +1475,7 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     iqo_amd::build_up2(h.p, h.wt, &h.ut);
     iqo_amd::build_d32(h.p, h.wt, &h.dt);
     iqo_amd::build_a32(h.p, &h.at);
+    iqo_amd::build_u23(h.p, &h.vt);
     return plan_kernel(&h);
 }
 

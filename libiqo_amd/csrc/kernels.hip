@@ -2517,6 +2517,223 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     }
 }
 
+// ================================================================ exact 2:3 Lanczos-3 upscale
+//
+// Lanczos-3 at exactly 3/2 (e.g. 1280x720 -> 1920x1080; plan.cpp build_u23).  Output y = 3m + j
+// takes phase j of the reference's table: j = 0 a single tap on source row 2m, j = 1 six taps from
+// 2m - 2, j = 2 six taps from 2m - 1 (IQOLanczosResizerImpl_Generic.cpp:144-190, 404-454; the
+// masked borders :464-490, :539-574 the same way as lanczos_d32_kernel: zero rows / columns outside
+// the image, border rows divided before the horizontal pass, the edge lanes' 12 sums parked and
+// rewritten once per trip).  One WAVE per (row band, output strip, frame); lane l (1..np) owns
+// source columns [cb, cb + 8) and output columns [3cb/2, 3cb/2 + 12); a group of 3 output rows adds
+// 2 source rows to a register window of 8 (4 groups per trip); 12-byte stores.
+struct U23Args {
+    U23Dev d;
+    Io io;
+    int rowBegin, rowEnd, row3Begin, rowsPerBand, bands, wavesPerRow, np;
+    int srcBytes, dstBytes;
+    unsigned nWaves;
+};
+
+template <int PD>
+__global__ __launch_bounds__(256) void lanczos_u23_kernel(U23Args a)
+{
+    constexpr int NW = 8, U = 4, OOB = 0x7ff00000;
+    static_assert(U % PD == 0, "prefetch slots repeat within a trip");
+    const U23Dev &d = a.d;
+    __shared__ int4 park[4][2][3 * U][3];  // per wave, side, row slot: the edge lane's 12 raw sums
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;
+    const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
+    const unsigned rest = gw / static_cast<unsigned>(a.wavesPerRow);
+    const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
+    const int yb = a.row3Begin + band * a.rowsPerBand;  // a multiple of 3
+    const int y0 = max(yb, a.rowBegin), y1 = min(yb + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int kLo = yb / 3;
+    const int nG = (y1 - yb + 2) / 3;
+
+    const int opw = 12 * a.np;
+    const int x0 = max(0, min(wcol * opw, d.dstW - opw));
+    const int cb = (2 * x0) / 3 - 8 + 8 * lane;
+    const bool produce = lane >= 1 && lane <= a.np;
+    const int voff = (lane <= a.np + 1 && cb >= 0 && cb + 8 <= d.srcW) ? cb : OOB;
+    const int stoff = produce ? x0 + 12 * (lane - 1) : OOB;
+    const bool edgeL = x0 == 0, edgeR = x0 + opw >= d.dstW;
+    const bool laneL = edgeL && lane == 1, laneR = edgeR && lane == a.np;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+
+    // relative source row q = row 2 kLo - 2 + q: zero outside the image, clamped outside the call's
+    // window (dropped outputs only), not loaded past the band's last group
+    const int rBase = 2 * kLo - 2;
+    const int rLast = 2 * (kLo + nG - 1) + 4;
+    const int srcLast = a.io.srcRowEnd - 1;
+    auto load_row = [&](int q) -> u32x2 {
+        const int r = rBase + q;
+        const int rc = min(max(r, srcRow0), srcLast);
+        const bool in = r >= 0 && r < d.srcH && r <= rLast;
+        return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](u32x2 v, uint32_t (&P)[4]) {
+        P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);
+        P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
+        P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
+        P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);
+    };
+    auto store_row = [&](u32x3 o, int voffs, int y, bool ok) {
+        __builtin_amdgcn_raw_buffer_store_b96(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+    };
+    auto border_row = [&](uint32_t (&W)[4], int y) {
+        if (y < d.m0 || y >= d.m1) {
+            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
+            const uint32_t m = d.yM[side][i];
+            const int sh = d.yS[side][i];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                W[c] = ydiv2(W[c], m, sh);
+        }
+    };
+    auto emit = [&](const uint32_t (&W)[4], int y, int slot) {
+        uint32_t E[7];  // E[e] = work columns (cb - 2 + 2e, cb - 1 + 2e)
+        E[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[3]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            E[e + 1] = W[e];
+        E[5] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[0]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        E[6] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[1]), 0x130, 0xf, 0xf, true));
+        uint32_t O[6];  // O[e] = work columns (cb - 1 + 2e, cb + 2e)
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+            O[e] = __builtin_amdgcn_alignbit(E[e + 1], E[e], 16);
+        auto pair = [&](int rel) { return (rel & 1) ? O[(rel + 1) / 2] : E[(rel + 2) / 2]; };  // low half = column cb + rel
+        int sum[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) {
+            const int g = j / 3, ph = j % 3;
+            if (ph == 0) {
+                sum[j] = sdot2(pair(2 * g), d.cx0, 1 << 19);
+            } else {
+                const int rel = 2 * g - 2 + (ph - 1);
+                int acc = sdot2(pair(rel), d.cx[ph - 1][0], 1 << 19);
+#pragma unroll
+                for (int q = 1; q < 3; ++q)
+                    acc = sdot2(pair(rel + 2 * q), d.cx[ph - 1][q], acc);
+                sum[j] = acc;
+            }
+        }
+        u32x3 o;
+        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+        o.z = pack_hi(pack_lo(sum[8], sum[9]), sum[10], sum[11]);
+        store_row(o, stoff, y, y >= y0 && y < y1);
+        if (edgeL || edgeR) {  // uniform
+            if (laneL || laneR) {
+                int4 *pk = park[wib][laneL ? 0 : 1][slot];
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    pk[q] = make_int4(sum[4 * q], sum[4 * q + 1], sum[4 * q + 2], sum[4 * q + 3]);
+            }
+        }
+    };
+    // once per trip: lane r < 3U rewrites the edge bytes of row yt + r from the parked sums
+    auto flush = [&](int yt) {
+        u32x3 oL = {0u, 0u, 0u}, oR = {0u, 0u, 0u};
+        const int r = min(lane, 3 * U - 1);
+        if (edgeL || edgeR) {  // uniform
+            __builtin_amdgcn_wave_barrier();
+            auto fix = [&](int side) {
+                uint32_t w[3];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int4 p = park[wib][side][r][q];
+                    const int sv[4] = {p.x, p.y, p.z, p.w};
+                    uint32_t b[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        b[e] = min(__umulhi(static_cast<uint32_t>(max(sv[e], 0)), d.xM[side][4 * q + e]) >> d.xT[side][4 * q + e],
+                                   255u);
+                    w[q] = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+                }
+                return u32x3{w[0], w[1], w[2]};
+            };
+            if (edgeL)
+                oL = fix(0);
+            if (edgeR)
+                oR = fix(1);
+        }
+        const int y = yt + lane;
+        const bool ok = lane < 3 * U && y >= y0 && y < y1;
+        store_row(oL, edgeL ? 0 : OOB, y, ok);
+        store_row(oR, edgeR ? d.dstW - 12 : OOB, y, ok);
+    };
+
+    uint32_t R[NW][4];
+    // group 0's window without its own new rows: relative rows 0..4
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+        widen(load_row(q), R[q]);
+    // prefetch: group g adds relative rows 2g + 5, 2g + 6
+    u32x2 pre[PD][2];
+#pragma unroll
+    for (int v = 0; v < PD; ++v) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            pre[v][i] = load_row(2 * v + 5 + i);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)  // the loop's three row stores per group, dropped
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{0u, 0u, 0u}, dstR, OOB, 0, 0);
+    }
+    __builtin_amdgcn_raw_buffer_store_b96(u32x3{0u, 0u, 0u}, dstR, OOB, 0, 0);  // and the trip's two flush stores
+    __builtin_amdgcn_raw_buffer_store_b96(u32x3{0u, 0u, 0u}, dstR, OOB, 0, 0);
+    for (int base = 0; base < nG; base += U) {
+        static_for<U>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int g = base + v;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                widen(pre[v % PD][i], R[(2 * v + 5 + i) % NW]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                pre[v % PD][i] = load_row(2 * (g + PD) + 5 + i);
+            const int y = 3 * (kLo + g);
+            uint32_t W[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)  // phase 0: source row 2m (relative 2g + 2)
+                W[c] = pk_mul(R[(2 * v + 2) % NW][c], d.cy0);
+            border_row(W, y);
+            emit(W, y, 3 * v);
+#pragma unroll
+            for (int ph = 0; ph < 2; ++ph) {  // phases 1, 2: six rows from relative 2g + ph
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    W[c] = pk_mul(R[(2 * v + ph) % NW][c], d.cy[ph][0]);
+#pragma unroll
+                for (int k = 1; k < 6; ++k)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c)
+                        W[c] = pk_mad(R[(2 * v + ph + k) % NW][c], d.cy[ph][k], W[c]);
+                border_row(W, y + 1 + ph);
+                emit(W, y + 1 + ph, 3 * v + 1 + ph);
+            }
+        });
+        flush(3 * (kLo + base));
+    }
+}
+
 // ================================================================ exact 3:2 Area downscale
 //
 // Area at exactly 2/3 (plan.cpp build_a32; the reference's Area tables for this ratio,
@@ -2982,6 +3199,44 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     if (nWaves >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     D32Args a{d, io, rowBegin, rowEnd, evenBegin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nWaves)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
+}
+
+hipError_t launch_u23(const U23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.dstW % 12 || d.dstW < 24 || 3 * d.srcW != 2 * d.dstW)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    const int lanes = d.dstW / 12;
+    int wpr = (lanes + 61) / 62;
+    int np = d.np > 0 ? min(d.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
+    const void *kern = d.pd == 2 ? reinterpret_cast<const void *>(lanczos_u23_kernel<2>)
+                                 : reinterpret_cast<const void *>(lanczos_u23_kernel<1>);
+    const int row3Begin = rowBegin - rowBegin % 3;
+    const int rows = rowEnd - row3Begin;
+    constexpr int trip = 12;  // output rows per unrolled trip
+    // bands: ~2.5 rounds of resident waves, whole trips per band, >= 24 rows
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
+        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 24)));
+    }
+    bands = std::max(1, std::min(bands, (rows + trip - 1) / trip));
+    int rpb = (rows + bands - 1) / bands;
+    rpb = (rpb + trip - 1) / trip * trip;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    U23Args a{d, io, rowBegin, rowEnd, row3Begin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nWaves)};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);

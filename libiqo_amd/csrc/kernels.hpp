@@ -97,6 +97,21 @@ struct D32Dev {
 };
 hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
+// Exact 2:3 Lanczos-3 upscale (plan.hpp U23Tables).
+struct U23Dev {
+    int srcW, srcH, dstW, dstH;
+    int np;                      // producing lanes per wave (0 = auto)
+    int pd;                      // row groups loaded ahead (1, 2; 0 = default 1)
+    uint32_t cy0, cy[2][6];      // (c, c) u16 splats: phase 0's tap, phases 1 and 2
+    uint32_t cx0, cx[2][3];      // (c, 0) / (c_2q, c_2q+1) int16 pairs
+    uint32_t xM[2][12];          // edge-lane exact divisions (left / right 12 columns)
+    int xT[2][12];
+    int m0, m1;                  // main rows; the others are masked border rows
+    uint32_t yM[2][8];
+    int yS[2][8];
+};
+hipError_t launch_u23(const U23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
 // Exact 3:2 Area downscale (plan.hpp A32Tables).
 struct A32Dev {
     int srcW, srcH, dstW, dstH;

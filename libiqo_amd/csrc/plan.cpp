@@ -1034,6 +1034,83 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
     u->ok = true;
 }
 
+void build_u23(const Plan &p, U23Tables *u)
+{
+    *u = U23Tables();
+    if (p.method != kLanczos || p.x.identity || p.y.identity || 3 * p.srcW != 2 * p.dstW || 3 * p.srcH != 2 * p.dstH ||
+        p.dstW % 12 || p.dstW < 24 || p.dstH < 12 || p.x.taps != 6 || p.y.taps != 6)
+        return;
+    // every window: start 2 (i / 3) - 2 + (i % 3 == 2), phase i % 3, phase 0 a single centre tap
+    auto fixed = [&](const AxisPlan &ax, int i, std::vector<int32_t> (&set)[3]) {
+        const CoordInfo &ci = ax.coord[static_cast<size_t>(i)];
+        if (ci.kind == kIdentity || ci.srcO != 2 * (i / 3) - 2 + (i % 3 == 2 ? 1 : 0) || ci.tabOff % 6 != 0)
+            return false;
+        const std::vector<int32_t> c(ax.table.begin() + ci.tabOff, ax.table.begin() + ci.tabOff + 6);
+        std::vector<int32_t> &ref = set[i % 3];
+        if (ref.empty())
+            ref = c;
+        return ref == c;
+    };
+    std::vector<int32_t> xs[3], ys[3];
+    for (int x = 0; x < p.dstW; ++x) {
+        if (!fixed(p.x, x, xs))
+            return;
+        const Window win = axis_window(p, p.x, x, true);
+        const int side = x < 12 ? 0 : x >= p.dstW - 12 ? 1 : -1;
+        if (win.border && side < 0)
+            return;
+        if (side >= 0) {
+            const int j = side ? x - (p.dstW - 12) : x;
+            if (!magic_x(win.border ? win.div : (1 << 20), &u->xM[side][j], &u->xT[side][j]))
+                return;
+        }
+    }
+    int m0 = -1, m1 = -1;
+    for (int y = 0; y < p.dstH; ++y) {
+        if (!fixed(p.y, y, ys))
+            return;
+        const Window win = axis_window(p, p.y, y, false);
+        if (!win.border) {
+            if (m0 < 0)
+                m0 = y;
+            else if (m1 >= 0)
+                return;
+        } else if (m0 >= 0 && m1 < 0) {
+            m1 = y;
+        }
+    }
+    if (m0 < 0)
+        return;
+    if (m1 < 0)
+        m1 = p.dstH;
+    if (m0 > 8 || p.dstH - m1 > 8)
+        return;
+    for (int y = 0; y < p.dstH; ++y) {
+        if (y >= m0 && y < m1)
+            continue;
+        const Window win = axis_window(p, p.y, y, false);
+        const int side = y < m0 ? 0 : 1, i = side ? y - m1 : y;
+        if (!magic_y(win.div, &u->yM[side][i], &u->yS[side][i]))
+            return;
+    }
+    for (int k = 0; k < 6; ++k)
+        if ((k == 2) != (ys[0][static_cast<size_t>(k)] != 0) || (k == 2) != (xs[0][static_cast<size_t>(k)] != 0))
+            return;
+    auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
+    u->cy0 = splat(ys[0][2]);
+    u->cx0 = static_cast<uint32_t>(xs[0][2]) & 0xffffu;
+    for (int ph = 0; ph < 2; ++ph) {
+        for (int k = 0; k < 6; ++k)
+            u->cy[ph][k] = splat(ys[ph + 1][static_cast<size_t>(k)]);
+        for (int q = 0; q < 3; ++q)
+            u->cx[ph][q] = (static_cast<uint32_t>(xs[ph + 1][static_cast<size_t>(2 * q)]) & 0xffffu) |
+                           (static_cast<uint32_t>(xs[ph + 1][static_cast<size_t>(2 * q + 1)]) << 16);
+    }
+    u->m0 = m0;
+    u->m1 = m1;
+    u->ok = true;
+}
+
 void build_a32(const Plan &p, A32Tables *t)
 {
     *t = A32Tables();

@@ -226,6 +226,24 @@ struct D32Tables {
 };
 void build_d32(const Plan &p, const WalkTables &w, D32Tables *d);
 
+// Exact 2:3 Lanczos-3 upscale (kernels.hip lanczos_u23_kernel), e.g. 1280x720 -> 1920x1080.  In the
+// reference's tables for this ratio output y (x) = 3m + j takes phase j: j = 0 a single tap on
+// source row 2m, j = 1 six taps from 2m - 2, j = 2 six taps from 2m - 1 (at the masked borders
+// too).  A group of 3 output rows reads source rows 2m - 2 .. 2m + 4 and adds 2 of them.
+struct U23Tables {
+    bool ok = false;
+    int m0 = 0, m1 = 0;             // main rows; the others are masked border rows
+    uint32_t cy0 = 0;               // (c, c) splat of phase 0's single tap
+    uint32_t cy[2][6] = {};         // (c, c) splats of phases 1 and 2
+    uint32_t cx0 = 0;               // (c, 0) pair of phase 0's tap
+    uint32_t cx[2][3] = {};         // phases 1, 2: (c_2q, c_2q+1) int16 pairs
+    uint32_t xM[2][12] = {};        // edge lanes (left: columns 0..11, right: dstW - 12 ..)
+    int32_t xT[2][12] = {};
+    uint32_t yM[2][8] = {};         // border row y (top: y, bottom: y - m1)
+    int32_t yS[2][8] = {};
+};
+void build_u23(const Plan &p, U23Tables *t);
+
 // Exact 3:2 Area downscale (kernels.hip area_d32_kernel), e.g. 1920x1080 -> 1280x720: output y (x)
 // takes the 2 non-zero taps of phase y & 1 starting at 3 (y >> 1) + (y & 1) (the third tap of the
 // reference's table is 0), so a row pair reads exactly the 3 source rows 3m .. 3m + 2 and a lane's

@@ -37,7 +37,7 @@ uint8_t edge_div(int s, uint32_t m, int t)
 
 extern "C" {
 
-// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32.  Returns 0 on success, 1 if the shape is
+// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23.  Returns 0 on success, 1 if the shape is
 // not eligible for that kernel, -1 on bad arguments.
 int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int dstW, int dstH, int pxScale,
                const uint8_t *src, uint8_t *dst)
@@ -125,6 +125,45 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
                 const int side = x < 16 ? 0 : x >= dstW - 16 ? 1 : -1;
                 dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(
                     side < 0 ? sat_u8(s >> 20) : edge_div(s, u.xM[side][side ? x - (dstW - 16) : x], u.xT[side][side ? x - (dstW - 16) : x]));
+            }
+        }
+        return 0;
+    }
+    if (kind == 3) {
+        U23Tables u;
+        build_u23(p, &u);
+        if (!u.ok)
+            return 1;
+        for (int y = 0; y < dstH; ++y) {
+            const int m = y / 3, ph = y % 3;
+            for (int c = 0; c < srcW; ++c) {
+                uint16_t acc = 0;
+                if (ph == 0)
+                    acc = static_cast<uint16_t>(px(2 * m, c) * static_cast<uint16_t>(u.cy0));
+                else
+                    for (int k = 0; k < 6; ++k)
+                        acc = static_cast<uint16_t>(acc + px(2 * m - 2 + (ph - 1) + k, c) * static_cast<uint16_t>(u.cy[ph - 1][k]));
+                if (y < u.m0 || y >= u.m1) {
+                    const int side = y < u.m0 ? 0 : 1, bi = side ? y - u.m1 : y;
+                    acc = ydiv1(acc, u.yM[side][bi], u.yS[side][bi]);
+                }
+                work[static_cast<size_t>(c)] = acc;
+            }
+            auto W = [&](int c) -> int { return (c < 0 || c >= srcW) ? 0 : static_cast<int16_t>(work[static_cast<size_t>(c)]); };
+            for (int x = 0; x < dstW; ++x) {
+                const int g = x / 3, q = x % 3;
+                int s = 1 << 19;
+                if (q == 0) {
+                    s += W(2 * g) * static_cast<int16_t>(u.cx0 & 0xffffu);
+                } else {
+                    const int a = 2 * g - 2 + (q - 1);
+                    for (int k = 0; k < 3; ++k)
+                        s += W(a + 2 * k) * static_cast<int16_t>(u.cx[q - 1][k] & 0xffffu) +
+                             W(a + 2 * k + 1) * static_cast<int16_t>(u.cx[q - 1][k] >> 16);
+                }
+                const int side = x < 12 ? 0 : x >= dstW - 12 ? 1 : -1;
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(
+                    side < 0 ? sat_u8(s >> 20) : edge_div(s, u.xM[side][side ? x - (dstW - 12) : x], u.xT[side][side ? x - (dstW - 12) : x]));
             }
         }
         return 0;

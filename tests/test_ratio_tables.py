@@ -17,7 +17,7 @@ import oracle_lib as ol
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
-KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2}
+KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3}
 
 
 @pytest.fixture(scope="module")
@@ -63,12 +63,14 @@ def test_ratio_tables_match_golden(emul, golden):
 def _shapes():
     rng = random.Random(32)
     out = [("lanczos_d32", "lanczos", 3, 1920, 1080, 1280, 720), ("lanczos_d32", "lanczos", 2, 1920, 1080, 1280, 720),
+           ("lanczos_u23", "lanczos", 3, 1280, 720, 1920, 1080),
            ("lanczos_up2", "lanczos", 3, 1920, 1080, 3840, 2160),
            ("area_d32", "area", 0, 1920, 1080, 1280, 720), ("lanczos_up2", "lanczos", 2, 200, 60, 400, 120)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_d32", "lanczos", 2, 12 * a, 3 * b, 8 * a, 2 * b))
+        out.append(("lanczos_u23", "lanczos", 3, 8 * a, 2 * b + 8, 12 * a, 3 * b + 12))
         out.append(("area_d32", "area", 0, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_up2", "lanczos", rng.choice((2, 3)), 8 * a, b + 4, 16 * a, 2 * b + 8))
     return out
