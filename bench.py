@@ -253,12 +253,19 @@ def main():
     if world != args.gpus:
         log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     dist = None
+    # IQO_BENCH_DIST=gloo rehearses the N>1 image-shard path with several ranks per GPU (rank r uses
+    # device r % device_count, control collectives over gloo); the real multi-GPU run uses RCCL
+    backend = os.environ.get("IQO_BENCH_DIST", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
+        torch.cuda.set_device(gpu)
         # control only: barriers and the MAX of the timings (band mode: the IPC handles); never pixels
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     cfg = CONFIGS[args.config]
@@ -276,7 +283,7 @@ def main():
             r.set_option(k, int(v))
         return r
 
-    r = make(local)
+    r = make(gpu)
     kernel = r.describe()["kernel"]
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
@@ -345,7 +352,8 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # events on the stream the kernels run on
 
-    t = torch.tensor([wall, t_sc if args.shard == "band" else 0.0], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, t_sc if args.shard == "band" else 0.0], dtype=torch.float64,
+                     device="cpu" if backend == "gloo" else dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # timing bookkeeping only, not the data path
     wall_max, scatter_max = float(t[0].item()), float(t[1].item())
