@@ -2075,6 +2075,9 @@ struct Up2Args {
 #ifndef IQO_D32_NT_STORE
 #define IQO_D32_NT_STORE 0
 #endif
+#ifndef IQO_A32_LOAD_NT
+#define IQO_A32_LOAD_NT 0
+#endif
 #ifndef IQO_A32_NT_STORE
 #define IQO_A32_NT_STORE 0
 #endif
@@ -2792,7 +2795,8 @@ __global__ __launch_bounds__(256) void area_d32_kernel(A32Args a)
     // used; rows past the band's last group are not loaded)
     auto load_row = [&](int r) -> u32x3 {
         const int rc = min(max(r, srcRow0), srcLast);
-        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0,
+                                                    IQO_A32_LOAD_NT ? 2 /* nt */ : 0);
     };
     auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
         P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);
