@@ -59,7 +59,8 @@ enum {
     IQO_KERNEL_LANCZOS_UP2 = 6, /* exact 2x Lanczos-2/3 upscale: register-window streamer + walker borders */
     IQO_KERNEL_LANCZOS_D32 = 7, /* exact 3:2 Lanczos-3 downscale: register-window streamer, borders in-kernel */
     IQO_KERNEL_AREA_D32 = 8,    /* exact 3:2 Area downscale: one wave per strip, no window */
-    IQO_KERNEL_LANCZOS_U23 = 9  /* exact 2:3 Lanczos-3 upscale: register-window streamer, borders in-kernel */
+    IQO_KERNEL_LANCZOS_U23 = 9, /* exact 2:3 Lanczos-3 upscale: register-window streamer, borders in-kernel */
+    IQO_KERNEL_LINEAR_U23 = 10  /* exact 2:3 Linear upscale: clamped halo, no border code */
 };
 
 typedef struct iqo_hip_plan iqo_hip_plan;
@@ -90,8 +91,8 @@ int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
  * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
  * IQO_KERNEL_GENERAL instead of IQO_KERNEL_TILE / _WALK), "walk" (0: IQO_KERNEL_TILE instead of
  * IQO_KERNEL_WALK / _LANCZOS_UP2; default 1), "up2" (0: IQO_KERNEL_WALK instead of
- * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" (0: IQO_KERNEL_WALK instead of
- * IQO_KERNEL_LANCZOS_D32 / IQO_KERNEL_AREA_D32 / IQO_KERNEL_LANCZOS_U23; default 1), "tile_rows" (output rows per tile, 0 = auto),
+ * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" / "l23" (0: IQO_KERNEL_WALK
+ * instead of IQO_KERNEL_LANCZOS_D32 / _AREA_D32 / _LANCZOS_U23 / _LINEAR_U23; default 1), "tile_rows" (output rows per tile, 0 = auto),
  * "prefetch", "lin_prefetch", "ratio_prefetch", "ring_pack", "stream_variant", "lanes",
  * "chunk_frames", "xcd_order" (A/B of
  * kernel variants and schedules, see libiqo_amd/csrc/abi.hip).  Every option changes speed only,

@@ -62,6 +62,9 @@ struct iqo_hip_plan {
     // exact 3:2 Lanczos-3 downscale kernel on the main rows (option "d32" = 0: walker only)
     iqo_amd::D32Tables dt;
     bool useD32 = true;
+    // exact 2:3 Linear upscale kernel (option "l23" = 0: walker only)
+    iqo_amd::L23Tables lt;
+    bool useL23 = false;  // off until the GPU parity run of linear_u23_kernel
     // exact 2:3 Lanczos-3 upscale kernel (option "u23" = 0: walker only)
     iqo_amd::U23Tables vt;
     bool useU23 = true;
@@ -383,6 +386,7 @@ int upload_tile(iqo_hip_plan *h)
     iqo_amd::build_d32(h->p, h->wt, &h->dt);
     iqo_amd::build_a32(h->p, &h->at);
     iqo_amd::build_u23(h->p, &h->vt);
+    iqo_amd::build_l23(h->p, &h->lt);
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
     for (size_t y = 0; y < t.rows.size(); ++y)
@@ -625,6 +629,20 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::L23Dev l23_dev(const iqo_hip_plan *h)
+{
+    iqo_amd::L23Dev d;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.np = h->lanes;
+    d.pd = h->ratioPrefetch;
+    std::memcpy(d.cy, h->lt.cy, sizeof d.cy);
+    std::memcpy(d.cx, h->lt.cx, sizeof d.cx);
+    return d;
+}
+
 iqo_amd::U23Dev u23_dev(const iqo_hip_plan *h)
 {
     const iqo_amd::U23Tables &t = h->vt;
@@ -698,6 +716,8 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_AREA_D32;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->vt.ok && h->useU23)
         k = IQO_KERNEL_LANCZOS_U23;
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->lt.ok && h->useL23)
+        k = IQO_KERNEL_LINEAR_U23;
     return k;
 }
 
@@ -735,6 +755,9 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->vt.ok && h->useU23 &&
         aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_U23;
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->lt.ok && h->useL23 &&
+        aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_LINEAR_U23;
     return kernel;
 }
 
@@ -810,6 +833,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_a32(a32_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_LANCZOS_U23)
             e = iqo_amd::launch_u23(u23_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_LINEAR_U23)
+            e = iqo_amd::launch_l23(l23_dev(h), io, rb, re, h->bands, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
         if (e != hipSuccess)
@@ -947,6 +972,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "up2")) {  // 0: exact 2x Lanczos upscales use the wave walker alone
         h->useUp2 = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "l23")) {  // 0: exact 2:3 Linear upscales use the wave walker alone
+        h->useL23 = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "u23")) {  // 0: exact 2:3 Lanczos-3 upscales use the wave walker alone
@@ -1476,6 +1505,7 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     iqo_amd::build_d32(h.p, h.wt, &h.dt);
     iqo_amd::build_a32(h.p, &h.at);
     iqo_amd::build_u23(h.p, &h.vt);
+    iqo_amd::build_l23(h.p, &h.lt);
     return plan_kernel(&h);
 }
 

@@ -2737,6 +2737,146 @@ __global__ __launch_bounds__(256) void lanczos_u23_kernel(U23Args a)
     }
 }
 
+// ================================================================ exact 2:3 Linear upscale
+//
+// Linear at exactly 3/2 (e.g. 1280x720 -> 1920x1080; plan.cpp build_l23): output y = 3m + j takes
+// phase j's two taps from source row 2m + j - 1 (IQOLinearResizerImpl_Generic.cpp:157-208 tables,
+// :210-282 rows; u16 vertical blend, (s + 2^22) >> 23 horizontal, :327-346).  With the source
+// clamped to the image (rows by address, the halo columns of the frame's first / last lane by
+// per-lane byte-broadcast selectors) the same two taps give the reference's replicated border
+// pixels, so there is no border code.  Lane layout of lanczos_u23_kernel: 8 source columns ->
+// 12 outputs; a group of 3 output rows adds 2 source rows to a window of 4.
+struct L23Args {
+    L23Dev d;
+    Io io;
+    int rowBegin, rowEnd, row3Begin, rowsPerBand, bands, wavesPerRow, np;
+    int srcBytes, dstBytes;
+    unsigned nWaves;
+};
+
+template <int PD>
+__global__ __launch_bounds__(256) void linear_u23_kernel(L23Args a)
+{
+    constexpr int NW = 4, U = 2, OOB = 0x7ff00000;
+    static_assert(U % PD == 0, "prefetch slots repeat within a trip");
+    const L23Dev &d = a.d;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;
+    const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
+    const unsigned rest = gw / static_cast<unsigned>(a.wavesPerRow);
+    const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
+    const int yb = a.row3Begin + band * a.rowsPerBand;
+    const int y0 = max(yb, a.rowBegin), y1 = min(yb + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int kLo = yb / 3;
+    const int nG = (y1 - yb + 2) / 3;
+
+    const int opw = 12 * a.np;
+    const int x0 = max(0, min(wcol * opw, d.dstW - opw));
+    const int cb = (2 * x0) / 3 - 8 + 8 * lane;
+    const bool produce = lane >= 1 && lane <= a.np;
+    // the halo lane left of column 0 / right of the last column replicates the edge pixel
+    const bool clampL = lane <= a.np + 1 && cb < 0, clampR = lane <= a.np + 1 && cb + 8 > d.srcW;
+    const int voff = lane > a.np + 1 ? OOB : clampL ? 0 : clampR ? d.srcW - 8 : cb;
+    const uint32_t selA = clampL ? 0x0c000c00u : clampR ? 0x0c070c07u : 0x0c010c00u;
+    const uint32_t selB = clampL ? 0x0c000c00u : clampR ? 0x0c070c07u : 0x0c030c02u;
+    const uint32_t selC = clampL ? 0x0c000c00u : clampR ? 0x0c070c07u : 0x0c050c04u;
+    const uint32_t selD = clampL ? 0x0c000c00u : clampR ? 0x0c070c07u : 0x0c070c06u;
+    const int stoff = produce ? x0 + 12 * (lane - 1) : OOB;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+
+    // relative source row q = row 2 kLo - 1 + q, clamped to the image (replicated border rows) and
+    // to the call's window (rows of dropped outputs only); not loaded past the band's last group
+    const int rBase = 2 * kLo - 1;
+    const int rLast = 2 * (kLo + nG - 1) + 2;
+    const int rMin = max(0, srcRow0), rMax = min(d.srcH - 1, a.io.srcRowEnd - 1);
+    auto load_row = [&](int q) -> u32x2 {
+        const int r = rBase + q;
+        const int rc = min(max(r, rMin), rMax);
+        return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](u32x2 v, uint32_t (&P)[4]) {
+        P[0] = __builtin_amdgcn_perm(v.y, v.x, selA);
+        P[1] = __builtin_amdgcn_perm(v.y, v.x, selB);
+        P[2] = __builtin_amdgcn_perm(v.y, v.x, selC);
+        P[3] = __builtin_amdgcn_perm(v.y, v.x, selD);
+    };
+    auto emit = [&](const uint32_t (&W)[4], int y) {
+        uint32_t E[6];  // E[e] = work columns (cb - 2 + 2e, cb - 1 + 2e)
+        E[0] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[3]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            E[e + 1] = W[e];
+        E[5] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(W[0]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        uint32_t O[5];  // O[e] = work columns (cb - 1 + 2e, cb + 2e)
+#pragma unroll
+        for (int e = 0; e < 5; ++e)
+            O[e] = __builtin_amdgcn_alignbit(E[e + 1], E[e], 16);
+        const uint32_t b = 1u << 22;
+        uint32_t sum[12];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            sum[3 * g] = udot2(O[g], d.cx[0], b);          // columns 2g - 1, 2g
+            sum[3 * g + 1] = udot2(E[g + 1], d.cx[1], b);  // 2g, 2g + 1
+            sum[3 * g + 2] = udot2(O[g + 1], d.cx[2], b);  // 2g + 1, 2g + 2
+        }
+        u32x3 o;
+        o.x = pack23_hi(pack23_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack23_hi(pack23_lo(sum[4], sum[5]), sum[6], sum[7]);
+        o.z = pack23_hi(pack23_lo(sum[8], sum[9]), sum[10], sum[11]);
+        __builtin_amdgcn_raw_buffer_store_b96(o, dstR, stoff + (y >= y0 && y < y1 ? (y - dstRow0) * dstSt : OOB), 0, 0);
+    };
+
+    uint32_t R[NW][4];
+    widen(load_row(0), R[0]);
+    widen(load_row(1), R[1]);
+    u32x2 pre[PD][2];
+#pragma unroll
+    for (int v = 0; v < PD; ++v) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            pre[v][i] = load_row(2 * v + 2 + i);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)  // the loop's three row stores per group, dropped
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{0u, 0u, 0u}, dstR, OOB, 0, 0);
+    }
+    for (int base = 0; base < nG; base += U) {
+        static_for<U>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int g = base + v;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                widen(pre[v % PD][i], R[(2 * v + 2 + i) % NW]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                pre[v % PD][i] = load_row(2 * (g + PD) + 2 + i);
+            const int y = 3 * (kLo + g);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {  // phase j: relative rows 2g + j, 2g + j + 1
+                uint32_t W[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    W[c] = pk_mad(R[(2 * v + j + 1) % NW][c], d.cy[j][1], pk_mul(R[(2 * v + j) % NW][c], d.cy[j][0]));
+                emit(W, y + j);
+            }
+        });
+    }
+}
+
 // ================================================================ exact 3:2 Area downscale
 //
 // Area at exactly 2/3 (plan.cpp build_a32; the reference's Area tables for this ratio,
@@ -3241,6 +3381,44 @@ hipError_t launch_u23(const U23Dev &d, const Io &io, int rowBegin, int rowEnd, i
     if (nWaves >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     U23Args a{d, io, rowBegin, rowEnd, row3Begin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nWaves)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
+}
+
+hipError_t launch_l23(const L23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.dstW % 12 || d.dstW < 24 || 3 * d.srcW != 2 * d.dstW || d.srcW < 8)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    const int lanes = d.dstW / 12;
+    int wpr = (lanes + 61) / 62;
+    int np = d.np > 0 ? min(d.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
+    const void *kern = d.pd == 1 ? reinterpret_cast<const void *>(linear_u23_kernel<1>)
+                                 : reinterpret_cast<const void *>(linear_u23_kernel<2>);
+    const int row3Begin = rowBegin - rowBegin % 3;
+    const int rows = rowEnd - row3Begin;
+    constexpr int trip = 6;  // output rows per unrolled trip
+    // bands: ~6 rounds of resident waves (no border code, a 4-row window), whole trips per band
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
+        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((6 * resident + perBand - 1) / perBand, std::max(1, rows / 12)));
+    }
+    bands = std::max(1, std::min(bands, (rows + trip - 1) / trip));
+    int rpb = (rows + bands - 1) / bands;
+    rpb = (rpb + trip - 1) / trip * trip;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    L23Args a{d, io, rowBegin, rowEnd, row3Begin, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nWaves)};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);

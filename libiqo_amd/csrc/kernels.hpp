@@ -112,6 +112,16 @@ struct U23Dev {
 };
 hipError_t launch_u23(const U23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
+// Exact 2:3 Linear upscale (plan.hpp L23Tables).
+struct L23Dev {
+    int srcW, srcH, dstW, dstH;
+    int np;                      // producing lanes per wave (0 = auto)
+    int pd;                      // row groups loaded ahead (1, 2; 0 = default 2)
+    uint32_t cy[3][2];           // (c, c) u16 splats of phase j's two taps
+    uint32_t cx[3];              // phase j's (c_0, c_1) u16 pair
+};
+hipError_t launch_l23(const L23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
 // Exact 3:2 Area downscale (plan.hpp A32Tables).
 struct A32Dev {
     int srcW, srcH, dstW, dstH;

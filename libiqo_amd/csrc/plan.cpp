@@ -1111,6 +1111,53 @@ void build_u23(const Plan &p, U23Tables *u)
     u->ok = true;
 }
 
+void build_l23(const Plan &p, L23Tables *t)
+{
+    *t = L23Tables();
+    if (p.method != kLinear || p.x.identity || p.y.identity || 3 * p.srcW != 2 * p.dstW || 3 * p.srcH != 2 * p.dstH ||
+        p.dstW % 12 || p.dstW < 24 || p.dstH < 3 || p.x.taps != 2 || p.y.taps != 2 || p.x.phases != 3 || p.y.phases != 3)
+        return;
+    auto axis = [&](const AxisPlan &ax, std::vector<int32_t> (&set)[3]) {
+        for (int i = 0; i < ax.dstLen; ++i) {
+            const CoordInfo &ci = ax.coord[static_cast<size_t>(i)];
+            const int j = i % 3, start = 2 * (i / 3) + j - 1;
+            if (ci.kind == kIdentity)
+                return false;
+            if (ci.kind == kBorderLo) {  // replicate pixel 0: both clamped taps must land on it
+                if (start + 1 > 0)
+                    return false;
+                continue;
+            }
+            if (ci.kind == kBorderHi) {  // replicate the last pixel
+                if (start < ax.srcLen - 1)
+                    return false;
+                continue;
+            }
+            if (ci.srcO != start || ci.tabOff != 2 * j || start < 0 || start + 1 >= ax.srcLen)
+                return false;
+            const std::vector<int32_t> c(ax.table.begin() + ci.tabOff, ax.table.begin() + ci.tabOff + 2);
+            std::vector<int32_t> &ref = set[j];
+            if (ref.empty())
+                ref = c;
+            if (ref != c)
+                return false;
+        }
+        return !set[0].empty() && !set[1].empty() && !set[2].empty();
+    };
+    std::vector<int32_t> xs[3], ys[3];
+    if (!axis(p.x, xs) || !axis(p.y, ys))
+        return;
+    for (int j = 0; j < 3; ++j) {
+        // the clamped border taps must weigh the edge pixel as the reference's replicate does
+        if (xs[j][0] + xs[j][1] != (1 << 15) || ys[j][0] + ys[j][1] != 256)
+            return;
+        for (int k = 0; k < 2; ++k)
+            t->cy[j][k] = (static_cast<uint32_t>(ys[j][static_cast<size_t>(k)]) & 0xffffu) * 0x10001u;
+        t->cx[j] = (static_cast<uint32_t>(xs[j][0]) & 0xffffu) | (static_cast<uint32_t>(xs[j][1]) << 16);
+    }
+    t->ok = true;
+}
+
 void build_a32(const Plan &p, A32Tables *t)
 {
     *t = A32Tables();

@@ -244,6 +244,17 @@ struct U23Tables {
 };
 void build_u23(const Plan &p, U23Tables *t);
 
+// Exact 2:3 Linear upscale (kernels.hip linear_u23_kernel), e.g. 1280x720 -> 1920x1080: output
+// y (x) = 3m + j takes phase j's two taps from source 2m + j - 1.  With the source clamped to the
+// image the same formula gives the reference's replicated border pixels (the coordinates it marks
+// as borders have both taps on the edge pixel), so the kernel has no border code.
+struct L23Tables {
+    bool ok = false;
+    uint32_t cy[3][2] = {};         // (c, c) u16 splats of phase j's two taps
+    uint32_t cx[3] = {};            // phase j's (c_0, c_1) u16 pair
+};
+void build_l23(const Plan &p, L23Tables *t);
+
 // Exact 3:2 Area downscale (kernels.hip area_d32_kernel), e.g. 1920x1080 -> 1280x720: output y (x)
 // takes the 2 non-zero taps of phase y & 1 starting at 3 (y >> 1) + (y & 1) (the third tap of the
 // reference's table is 0), so a row pair reads exactly the 3 source rows 3m .. 3m + 2 and a lane's

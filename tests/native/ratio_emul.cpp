@@ -168,6 +168,29 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
         }
         return 0;
     }
+    if (kind == 4) {
+        L23Tables l;
+        build_l23(p, &l);
+        if (!l.ok)
+            return 1;
+        auto cl = [&](int r, int c) {
+            r = r < 0 ? 0 : (r >= srcH ? srcH - 1 : r);
+            c = c < 0 ? 0 : (c >= srcW ? srcW - 1 : c);
+            return static_cast<int>(src[static_cast<size_t>(r) * srcW + c]);
+        };
+        for (int y = 0; y < dstH; ++y) {
+            const int m = y / 3, j = y % 3, r0 = 2 * m + j - 1;
+            std::vector<uint16_t> wrow(static_cast<size_t>(srcW) + 2);
+            auto Wc = [&](int c) { return static_cast<uint32_t>(static_cast<uint16_t>(
+                                       cl(r0, c) * static_cast<uint16_t>(l.cy[j][0]) + cl(r0 + 1, c) * static_cast<uint16_t>(l.cy[j][1]))); };
+            for (int x = 0; x < dstW; ++x) {
+                const int g = x / 3, q = x % 3, a = 2 * g + q - 1;
+                const uint32_t s = (1u << 22) + Wc(a) * (l.cx[q] & 0xffffu) + Wc(a + 1) * (l.cx[q] >> 16);
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(sat_u8(static_cast<int>(s) >> 23));
+            }
+        }
+        return 0;
+    }
     if (kind == 2) {
         A32Tables a;
         build_a32(p, &a);

@@ -51,7 +51,7 @@ def test_golden_vectors_gpu(golden, variant):
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
         if variant == "tile":
-            for k in ("walk", "a32", "d32", "up2", "u23"):
+            for k in ("walk", "a32", "d32", "up2", "u23", "l23"):
                 r.set_option(k, 0)
         elif variant != "default":
             r.set_option(variant, 1)
@@ -383,11 +383,11 @@ def test_tile_streamer_matches_oracle(cfg):
     frames[1, :, : sw // 3] = 255
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
     t = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    for k in ("walk", "a32", "d32", "up2", "u23"):
+    for k in ("walk", "a32", "d32", "up2", "u23", "l23"):
         t.set_option(k, 0)
     assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    for k in ("up2", "d32", "a32", "u23"):  # exact-ratio kernels off: the walker alone (their own tests below)
+    for k in ("up2", "d32", "a32", "u23", "l23"):  # exact-ratio kernels off: the walker alone (their own tests below)
         r.set_option(k, 0)
     kern = r.describe()["kernel"]
     assert kern in ("walk", "tile")
@@ -400,7 +400,7 @@ def test_tile_streamer_matches_oracle(cfg):
     if kern == "walk":
         for bands in (1, 3, 7, dh):
             w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-            for k in ("up2", "d32", "a32", "u23"):
+            for k in ("up2", "d32", "a32", "u23", "l23"):
                 w.set_option(k, 0)
             w.set_option("bands", bands)
             out = w.resize_tensor(src).cpu().numpy()
@@ -907,6 +907,65 @@ def test_lanczos_u23_matches_oracle(cfg):
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
     for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 5), ("lanes", 62)):
         b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option(opt, val)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = [0, 4, dh // 3 + 1, dh // 2, dh - 5, dh]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    sst, dst_st = sw + 8, dw + 4
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 9, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
+    assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
+    dst = torch.zeros((n, dh, dw + 2), dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 2, dh * (dw + 2), dst.data_ptr())
+    torch.cuda.synchronize()
+    assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+
+
+L23_SHAPES = [
+    ("linear", 0, 1280, 720, 1920, 1080, 1),     # 720p -> 1080p: three waves per row (x0 of the last clamped)
+    ("linear", 0, 640, 360, 960, 540, 1),        # two waves per row
+    ("linear", 0, 160, 100, 240, 150, 1),        # one wave holding both edges
+]
+
+
+@pytest.mark.parametrize("cfg", L23_SHAPES, ids=lambda c: "%s%d_%dx%d" % c[:4])
+def test_linear_u23_matches_oracle(cfg):
+    """Exact 2:3 Linear upscale: linear_u23_kernel on every row and column (the replicated borders
+    from the clamped source); equal to the oracle on noise, flat and half-flat frames;
+    with option l23 = 0 (walker alone), in band splits and lane counts, in row bands through their
+    source windows (odd band edges), with padded strides (l23 again) and a destination stride that
+    is not 4-byte aligned (walker / tile)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    n = 3
+    frames = _noise_batch(n, sw, sh, 2100)
+    frames[1] = 77
+    frames[2, :, : sw // 2] = 255
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    r.set_option("l23", 1)
+    assert r.describe()["kernel"] == "linear_u23"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    w.set_option("l23", 0)
+    assert w.describe()["kernel"] in ("walk", "tile")
+    assert (w.resize_tensor(src).cpu().numpy() == out).all()
+    for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 5), ("lanes", 62)):
+        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option("l23", 1)
         b.set_option(opt, val)
         assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
     got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)

@@ -17,7 +17,7 @@ import oracle_lib as ol
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
-KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3}
+KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4}
 
 
 @pytest.fixture(scope="module")
@@ -64,6 +64,7 @@ def _shapes():
     rng = random.Random(32)
     out = [("lanczos_d32", "lanczos", 3, 1920, 1080, 1280, 720), ("lanczos_d32", "lanczos", 2, 1920, 1080, 1280, 720),
            ("lanczos_u23", "lanczos", 3, 1280, 720, 1920, 1080),
+           ("linear_u23", "linear", 0, 1280, 720, 1920, 1080),
            ("lanczos_up2", "lanczos", 3, 1920, 1080, 3840, 2160),
            ("area_d32", "area", 0, 1920, 1080, 1280, 720), ("lanczos_up2", "lanczos", 2, 200, 60, 400, 120)]
     for _ in range(6):
@@ -71,6 +72,7 @@ def _shapes():
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_d32", "lanczos", 2, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_u23", "lanczos", 3, 8 * a, 2 * b + 8, 12 * a, 3 * b + 12))
+        out.append(("linear_u23", "linear", 0, 8 * a, 2 * b, 12 * a, 3 * b))
         out.append(("area_d32", "area", 0, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_up2", "lanczos", rng.choice((2, 3)), 8 * a, b + 4, 16 * a, 2 * b + 8))
     return out
