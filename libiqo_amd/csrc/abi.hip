@@ -64,7 +64,7 @@ struct iqo_hip_plan {
     bool useD32 = true;
     // exact 2:3 Linear upscale kernel (option "l23" = 0: walker only)
     iqo_amd::L23Tables lt;
-    bool useL23 = false;  // off until the GPU parity run of linear_u23_kernel
+    bool useL23 = true;
     // exact 2:3 Lanczos-3 upscale kernel (option "u23" = 0: walker only)
     iqo_amd::U23Tables vt;
     bool useU23 = true;

@@ -105,7 +105,7 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-2
     (("lanczos", 4, 1920, 1080, 1280, 720, 1), "walk"),
     (("lanczos", 3, 1280, 720, 1920, 1080, 1), "lanczos_u23"),    # exact 2:3 Lanczos-3 upscale
-    (("linear", 0, 1280, 720, 1920, 1080, 1), "walk"),            # exact 2:3 Linear: linear_u23 opt-in (l23)
+    (("linear", 0, 1280, 720, 1920, 1080, 1), "linear_u23"),      # exact 2:3 Linear upscale
     (("area", 0, 1920, 1080, 1280, 720, 1), "area_d32"),          # exact 3:2 Area: no window, no halo
     (("lanczos", 3, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-3: register window
     (("area", 0, 1921, 1080, 1280, 720, 1), "walk"),
