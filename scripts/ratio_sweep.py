@@ -3,7 +3,7 @@
 (distinct batches cycled, >= 2.5 GB per cycle, as bench.py), each output checked against the oracle
 on one frame.  Output: one line per shape (profiles/r02/ratio_sweep.txt).
 
-  python scripts/ratio_sweep.py [--steps 20]
+  python scripts/ratio_sweep.py [--steps 20] [--match linear:1280x720] [--opt ratio_prefetch=1 ...]
 """
 import argparse
 import os
@@ -36,6 +36,8 @@ SHAPES = [
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--match", default="", help="only shapes whose 'method:srcWxsrcH->dstWxdstH' contains this")
+    ap.add_argument("--opt", action="append", default=[], help="plan option key=value (tuning runs)")
     args = ap.parse_args()
     import torch
     import libiqo_amd
@@ -44,10 +46,15 @@ def main():
     s = torch.cuda.current_stream(dev)
     print("%-8s %-3s %-11s %-11s %-14s %9s %8s %7s %s" % ("method", "deg", "src", "dst", "kernel", "frames", "ms", "%peak", "parity"))
     for m, d, sw, sh, dw, dh in SHAPES:
+        if args.match not in "%s:%dx%d->%dx%d" % (m, sw, sh, dw, dh):
+            continue
         per = sw * sh + dw * dh
         frames = max(8, min(256, int(1.3e9 // per)))
         rot = max(2, int(-(-2.5e9 // (per * frames))))
         r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh)
+        for kv in args.opt:
+            k, v = kv.split("=")
+            r.set_option(k, int(v))
         kern = r.describe()["kernel"]
         src = torch.randint(0, 256, (rot, frames, sh, sw), dtype=torch.uint8, device=dev)
         dst = torch.empty((rot, frames, dh, dw), dtype=torch.uint8, device=dev)
