@@ -188,6 +188,10 @@ int iqo_host_band_src_rows(int method, unsigned degree, size_t srcW, size_t srcH
 int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                         size_t pxScale);
 
+/* Drop-in classes (include/libiqo/*Resizer.hpp): how many objects this process constructed on the
+ * HIP backend and on the CPU backend (no gfx950 device; IQO_REQUIRE_HIP=1 forbids it). */
+void iqo_dropin_backend_counts(int *hip, int *cpu);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2,8 +2,11 @@
 
 // Drop-in replacement of libiqo's iqo::LanczosResizer (include/libiqo/LanczosResizer.hpp:14-60):
 // same constructor and resize() signatures, output bytes identical to the reference's Generic
-// implementation.  Work runs on the current HIP device (gfx950); a HIP failure prints a message
-// and aborts (the reference API has no error channel and this library has no CPU fallback).
+// implementation.  Backend, chosen at construction like the reference's CPUID dispatch
+// (src/IQOLanczosResizer.cpp:15-36): the current HIP device when a gfx950 device is present,
+// otherwise the library's CPU restatement of Generic (libiqo_amd/csrc/cpu_generic.cpp).  A HIP
+// failure inside resize() prints one message and runs that call on the CPU path (the API has no
+// error channel).  IQO_REQUIRE_HIP=1 in the environment makes both fallbacks abort instead.
 
 #include <stddef.h>
 

@@ -1,19 +1,32 @@
 // resizers.cpp -- the reference's public classes (iqo::LanczosResizer / AreaResizer /
-// LinearResizer, include/libiqo/*.hpp) implemented on the HIP backend through the C ABI.
+// LinearResizer, include/libiqo/*.hpp) on the HIP backend, with the reference's fallback.
 //
 // Reference dispatch being replaced: src/IQOLanczosResizer.cpp:7-49 (and the Area / Linear
-// twins): CPUID probing + *ResizerImpl_new<Arch>() + m_Impl->init(); resize() forwards.  Here the
-// private impl object simply owns an iqo_hip_plan on the caller's current HIP device.
+// twins): CPUID probing, *ResizerImpl_new<Arch>() for the best compiled-in SIMD implementation,
+// Generic when none is available (:33), m_Impl->init(); resize() forwards.  Here:
+//   * a usable gfx950 device (iqo_hip_available() > 0) -> the impl owns an iqo_hip_plan on the
+//     caller's current HIP device (the GPU path every parity test and benchmark measures);
+//   * no device -> the impl owns the host plan and runs cpu_generic.cpp, the product's own CPU
+//     restatement (never the oracle), as the reference runs Generic;
+//   * a HIP error during resize() -> a one-time message on stderr, then the CPU path for that
+//     call (the public API has no error channel).
+// IQO_REQUIRE_HIP=1 in the environment turns both fallbacks into an abort: the GPU tests set it,
+// so a test can never pass on the CPU path by accident.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 
 #include <hip/hip_runtime_api.h>
 
+#include "cpu_generic.hpp"
 #include "iqo_hip.h"
 #include "libiqo/AreaResizer.hpp"
 #include "libiqo/DeviceResizer.hpp"
 #include "libiqo/LanczosResizer.hpp"
 #include "libiqo/LinearResizer.hpp"
+#include "plan.hpp"
 
 namespace iqo {
 
@@ -25,6 +38,12 @@ namespace {
     std::abort();
 }
 
+bool require_hip()
+{
+    const char *e = std::getenv("IQO_REQUIRE_HIP");
+    return e && *e && std::strcmp(e, "0") != 0;
+}
+
 int current_device()
 {
     int dev = 0;
@@ -33,15 +52,62 @@ int current_device()
     return dev;
 }
 
+std::atomic<int> g_cpuResizers{0}, g_hipResizers{0};
+std::atomic<bool> g_warned{false};
+
 struct PlanHolder {
-    iqo_hip_plan *plan = nullptr;
+    iqo_hip_plan *plan = nullptr;  // GPU backend, or
+    iqo_amd::Plan host;            // the CPU backend's plan (built when plan == nullptr)
+
     ~PlanHolder() { iqo_hip_plan_destroy(plan); }
+
+    // hipPlan: the iqo_hip_plan_* call for this method on device `dev`; hostPlan: build_plan
+    template <typename HipPlan, typename HostPlan>
+    void init(const char *what, HipPlan hipPlan, HostPlan hostPlan)
+    {
+        int rc = IQO_HIP_ENODEV;
+        if (iqo_hip_available() > 0)
+            rc = hipPlan(current_device(), &plan);
+        if (rc == 0) {
+            ++g_hipResizers;
+            return;
+        }
+        if (require_hip())
+            fatal(what, rc);
+        plan = nullptr;
+        std::string err;
+        if (!hostPlan(&host, &err)) {
+            std::fprintf(stderr, "libiqo_amd: %s: %s\n", what, err.c_str());
+            std::abort();
+        }
+        ++g_cpuResizers;
+    }
+
     void resize(size_t srcSt, const unsigned char *src, size_t dstSt, unsigned char *dst)
     {
-        int rc = iqo_hip_resize(plan, srcSt, src, dstSt, dst);
-        if (rc)
-            fatal("resize", rc);
+        if (plan) {
+            const int rc = iqo_hip_resize(plan, srcSt, src, dstSt, dst);
+            if (rc == 0)
+                return;
+            if (require_hip())
+                fatal("resize", rc);
+            if (!g_warned.exchange(true))
+                std::fprintf(stderr, "libiqo_amd: HIP resize failed (%s, %d); using the CPU path\n",
+                             iqo_hip_strerror(rc), rc);
+            if (host.dstW == 0) {
+                iqo_hip_plan_desc d;
+                std::string err;
+                if (iqo_hip_plan_query(plan, &d) != 0 ||
+                    !iqo_amd::build_plan(static_cast<iqo_amd::Method>(d.method), m_degree, d.srcW, d.srcH, d.dstW,
+                                         d.dstH, m_pxScale, &host, &err))
+                    fatal("resize (CPU fallback plan)", rc);
+            }
+        }
+        iqo_amd::cpu_resize(host, srcSt, src, dstSt, dst);
     }
+
+    unsigned m_degree = 0;
+    size_t m_pxScale = 1;
 };
 
 } // namespace
@@ -54,9 +120,14 @@ LanczosResizer::LanczosResizer(unsigned int degree, size_t srcW, size_t srcH, si
                                size_t pxScale)
     : m_Impl(new ILanczosResizerImpl())
 {
-    int rc = iqo_hip_plan_lanczos(degree, srcW, srcH, dstW, dstH, pxScale, current_device(), &m_Impl->plan);
-    if (rc)
-        fatal("LanczosResizer construction", rc);
+    m_Impl->m_degree = degree;
+    m_Impl->m_pxScale = pxScale;
+    m_Impl->init(
+        "LanczosResizer construction",
+        [&](int dev, iqo_hip_plan **p) { return iqo_hip_plan_lanczos(degree, srcW, srcH, dstW, dstH, pxScale, dev, p); },
+        [&](iqo_amd::Plan *p, std::string *e) {
+            return iqo_amd::build_plan(iqo_amd::kLanczos, degree, srcW, srcH, dstW, dstH, pxScale, p, e);
+        });
 }
 
 LanczosResizer::~LanczosResizer() { delete m_Impl; }
@@ -68,9 +139,12 @@ void LanczosResizer::resize(size_t srcSt, const unsigned char *src, size_t dstSt
 
 AreaResizer::AreaResizer(size_t srcW, size_t srcH, size_t dstW, size_t dstH) : m_Impl(new IAreaResizerImpl())
 {
-    int rc = iqo_hip_plan_area(srcW, srcH, dstW, dstH, current_device(), &m_Impl->plan);
-    if (rc)
-        fatal("AreaResizer construction", rc);
+    m_Impl->init(
+        "AreaResizer construction",
+        [&](int dev, iqo_hip_plan **p) { return iqo_hip_plan_area(srcW, srcH, dstW, dstH, dev, p); },
+        [&](iqo_amd::Plan *p, std::string *e) {
+            return iqo_amd::build_plan(iqo_amd::kArea, 0, srcW, srcH, dstW, dstH, 1, p, e);
+        });
 }
 
 AreaResizer::~AreaResizer() { delete m_Impl; }
@@ -82,9 +156,12 @@ void AreaResizer::resize(size_t srcSt, const unsigned char *src, size_t dstSt, u
 
 LinearResizer::LinearResizer(size_t srcW, size_t srcH, size_t dstW, size_t dstH) : m_Impl(new ILinearResizerImpl())
 {
-    int rc = iqo_hip_plan_linear(srcW, srcH, dstW, dstH, current_device(), &m_Impl->plan);
-    if (rc)
-        fatal("LinearResizer construction", rc);
+    m_Impl->init(
+        "LinearResizer construction",
+        [&](int dev, iqo_hip_plan **p) { return iqo_hip_plan_linear(srcW, srcH, dstW, dstH, dev, p); },
+        [&](iqo_amd::Plan *p, std::string *e) {
+            return iqo_amd::build_plan(iqo_amd::kLinear, 0, srcW, srcH, dstW, dstH, 1, p, e);
+        });
 }
 
 LinearResizer::~LinearResizer() { delete m_Impl; }
@@ -117,3 +194,13 @@ int DeviceResizer::resize(size_t nFrames, size_t srcSt, size_t srcFrameSt, const
 }
 
 } // namespace iqo
+
+// How many drop-in objects this process built on each backend (tests and the benchmark CLI report
+// it, so a run on the CPU path is visible).
+extern "C" void iqo_dropin_backend_counts(int *hip, int *cpu)
+{
+    if (hip)
+        *hip = iqo::g_hipResizers.load();
+    if (cpu)
+        *cpu = iqo::g_cpuResizers.load();
+}

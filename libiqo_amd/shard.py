@@ -117,6 +117,26 @@ def run_bands_distributed(backend, shards, rank, world, dist, clock=time.perf_co
     return {"scatter_s": t1 - t0, "compute_s": t2 - t1, "gather_s": t3 - t2}, band
 
 
+CopyOp = namedtuple("CopyOp", "dst dst_st src src_st nbytes count")
+
+
+def gather_ops(sh, src, src_fst, src_pitch, frames, dst, dst_fst, dst_pitch, width):
+    """Copy operations that move shard `sh`'s band into the root output.
+
+    The band holds output rows [r0, r1) of every frame at its OWN frame stride `src_fst` and row
+    pitch `src_pitch`; the output holds whole frames at `dst_fst` / `dst_pitch`.  Each CopyOp is
+    `count` blocks of `nbytes` (block k at dst + k*dst_st and src + k*src_st), the shape of
+    iqo_hip_copy_frames.  Equal pitches: one op, a band-sized block per frame.  Different
+    pitches: one op per frame, a `width`-byte block per row."""
+    rows = sh.r1 - sh.r0
+    if rows <= 0 or frames <= 0:
+        return []
+    if src_pitch == dst_pitch:
+        return [CopyOp(dst + sh.r0 * dst_pitch, dst_fst, src, src_fst, (rows - 1) * dst_pitch + width, frames)]
+    return [CopyOp(dst + f * dst_fst + sh.r0 * dst_pitch, dst_pitch, src + f * src_fst, src_pitch, width, rows)
+            for f in range(frames)]
+
+
 class HipBandBackend:
     """Row-band shards on gfx950 devices through the C ABI.
 
@@ -179,32 +199,35 @@ class HipBandBackend:
     def gather(self, sh, band):
         from . import copy_frames
 
-        rows = sh.r1 - sh.r0
         stream = self.torch.cuda.current_stream(self._dev(self.root))
-        p = copy_frames(self.out.data_ptr() + sh.r0 * self.dst_st, self.root, self.dst_fst, band.data_ptr(), sh.device,
-                        band.stride(0), rows * self.dst_st, self.frames, stream)
-        self._route("gather", p)
+        for op in gather_ops(sh, band.data_ptr(), band.stride(0), band.stride(1), self.frames, self.out.data_ptr(),
+                             self.dst_fst, self.dst_st, self.out.shape[2]):
+            p = copy_frames(op.dst, self.root, op.dst_st, op.src, sh.device, op.src_st, op.nbytes, op.count, stream)
+            self._route("gather", p)
 
     def gather_distributed(self, shards, band, rank, world, dist):
-        """Every rank exports its band's IPC handle (the handles travel over the control group,
-        the pixels never do); rank 0 opens each and pulls it by peer copy into `out`."""
+        """Every rank exports its band's IPC handle together with the band's frame stride and row
+        pitch (the handles travel over the control group, the pixels never do); rank 0 opens each
+        and pulls it by peer copy into `out`, with THAT band's strides: bands are uneven when
+        world does not divide dstH, and a rank without `out` allocates its band at pitch dstW."""
         from . import copy_frames, ipc_close, ipc_export, ipc_open
 
-        mine = ipc_export(band.data_ptr())
-        handles = [None] * world
-        dist.all_gather_object(handles, mine)
+        mine = (ipc_export(band.data_ptr()), band.stride(0), band.stride(1))
+        metas = [None] * world
+        dist.all_gather_object(metas, mine)
         if rank == 0:
             stream = self.torch.cuda.current_stream(self._dev(self.root))
             for sh in shards:
-                rows = sh.r1 - sh.r0
+                handle, fst, pitch = metas[sh.index]
                 if sh.index == 0:
                     src, h = band.data_ptr(), None
                 else:
-                    src, h = ipc_open(handles[sh.index], self.root)
-                p = copy_frames(self.out.data_ptr() + sh.r0 * self.dst_st, self.root, self.dst_fst, src,
-                                self.root if h is not None else sh.device, band.stride(0), rows * self.dst_st,
-                                self.frames, stream)
-                self._route("gather", p if h is None else "IPC-mapped peer buffer, copied by the root's DMA")
+                    src, h = ipc_open(handle, self.root)
+                for op in gather_ops(sh, src, fst, pitch, self.frames, self.out.data_ptr(), self.dst_fst, self.dst_st,
+                                     self.out.shape[2]):
+                    p = copy_frames(op.dst, self.root, op.dst_st, op.src, self.root if h is not None else sh.device,
+                                    op.src_st, op.nbytes, op.count, stream)
+                    self._route("gather", p if h is None else "IPC-mapped peer buffer, copied by the root's DMA")
                 if h is not None:
                     self.torch.cuda.synchronize(self._dev(self.root))
                     ipc_close(src, h)

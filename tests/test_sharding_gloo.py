@@ -106,7 +106,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_two_rank_image_and_band_sharding(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -150,3 +150,38 @@ def test_band_plan_covers_frame_and_halo_is_small():
     assert [shard.frame_range(10, r, 4) for r in range(4)] == [(0, 3), (3, 6), (6, 8), (8, 10)]
     shards = shard.make_shards(lambda r0, n: (r0, n), 10, [3, 5])
     assert shards == [shard.Shard(0, 3, 0, 5, 0, 5), shard.Shard(1, 5, 5, 10, 5, 10)]
+
+
+def _apply(ops, dst_buf, src_buf, src_base):
+    """Byte-level emulation of iqo_hip_copy_frames for gather_ops (addresses are offsets)."""
+    for op in ops:
+        for k in range(op.count):
+            d, s = op.dst + k * op.dst_st, op.src - src_base + k * op.src_st
+            dst_buf[d:d + op.nbytes] = src_buf[s:s + op.nbytes]
+
+
+@pytest.mark.parametrize("world,dh,root_pad", [(3, 31, 5), (3, 1081, 0), (7, 64, 3), (2, 60, 0)])
+def test_gather_ops_uneven_bands_and_padded_root(world, dh, root_pad):
+    """bands are uneven when world does not divide dstH and non-root ranks
+    allocate their bands at pitch dstW, so the root must copy each band with that band's own frame
+    stride and row pitch (HipBandBackend.gather / gather_distributed use gather_ops)."""
+    frames, dw = 3, 24
+    dst_pitch = dw + root_pad
+    ref = np.random.default_rng(dh).integers(0, 256, (frames, dh, dw), dtype=np.uint8)
+    out = np.zeros((frames, dh, dst_pitch), np.uint8)
+    shards = shard.make_shards(lambda r0, n: (r0, n), dh, list(range(world)))
+    assert len({s.r1 - s.r0 for s in shards}) == (1 if dh % world == 0 else 2)
+    flat = out.reshape(-1)
+    for sh in shards:
+        rows = sh.r1 - sh.r0
+        pitch = dst_pitch if sh.index == 0 else dw  # compute(): the root uses out's pitch, others dstW
+        band = np.zeros((frames, rows, pitch), np.uint8)
+        band[:, :, :dw] = ref[:, sh.r0:sh.r1]
+        base = 1 << 20  # the band's "address"
+        ops = shard.gather_ops(sh, base, rows * pitch, pitch, frames, 0, dh * dst_pitch, dst_pitch, dw)
+        _apply(ops, flat, band.reshape(-1), base)
+        for op in ops:  # every op stays inside the band and inside the output
+            assert op.src - base + (op.count - 1) * op.src_st + op.nbytes <= band.size
+            assert op.dst + (op.count - 1) * op.dst_st + op.nbytes <= out.size
+    assert (out[:, :, :dw] == ref).all()
+    assert (out[:, :, dw:] == 0).all()  # padding never written
