@@ -222,6 +222,29 @@ def reuse_probe(step_batch, rot, dev, reps=10):
     return {"same_batch_kernel_ms": round(same, 4), "rotated_kernel_ms": round(fresh, 4)}
 
 
+def alt_batch(make_step, frames_alt, bytes_per_frame, dev, steps=20, warmup=3):
+    """Kernel ms per launch at a second batch size, on rotated fresh batches like the headline
+    (BASELINE.md section 4 quotes C2 at >= 256 frames per launch; the headline uses C5's per-GPU
+    share of 128): same kernel, same plan, only the frame count differs."""
+    import torch
+
+    step, cleanup = make_step(frames_alt)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        step()
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    cleanup()
+    gbps = frames_alt * bytes_per_frame / (ms / 1e3) / 1e9
+    return {"frames": frames_alt, "kernel_ms_per_launch": round(ms, 4), "ms_per_frame": round(ms / frames_alt, 6),
+            "achieved": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -238,6 +261,8 @@ def main():
     ap.add_argument("--rotate", type=int, default=0,
                     help="distinct device batches cycled through, one per step (0 = auto: >= 2.5 GB per cycle, "
                          "10x the Infinity Cache, so no step re-reads the previous steps' data from it)")
+    ap.add_argument("--alt-frames", type=int, default=-1,
+                    help="also time this many frames per launch (rotated batches; -1 = 256 for c2, 0 = off)")
     ap.add_argument("--force-general", action="store_true")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="plan option (iqo_hip_plan_set_option), repeatable; speed-only A/B knobs")
@@ -326,10 +351,18 @@ def main():
         band = torch.empty((frames, rows, dw), dtype=torch.uint8, device=dev)
         bytes_launch = float(frames) * (srows * sw + rows * dw)
         out_px_step = float(frames) * dw * dh  # the whole frame, all ranks together
+        # like image mode, steps cycle through distinct copies of the window (>= 2.5 GB per cycle)
+        # so no step re-reads its input from the Infinity Cache; the uploaded window is copy 0
+        rot = args.rotate or max(2, int(-(-2.5e9 // bytes_launch)))
+        wins = [win] + [win.clone() for _ in range(rot - 1)]
+        bands_out = [band] + [torch.empty_like(band) for _ in range(rot - 1)]
+        nstep = [0]
 
         def step():
-            r.resize_band(frames, mine.r0, rows, mine.s0, sw, win.stride(0), win.data_ptr(), dw, band.stride(0),
-                          band.data_ptr(), sp)
+            b = nstep[0] % rot
+            nstep[0] += 1
+            r.resize_band(frames, mine.r0, rows, mine.s0, sw, wins[b].stride(0), wins[b].data_ptr(), dw,
+                          bands_out[b].stride(0), bands_out[b].data_ptr(), sp)
 
     log("rank %d/%d %s shard=%s frames=%d kernel=%s warmup=%d steps=%d" % (rank, world, label, args.shard, frames,
                                                                         kernel, args.warmup, args.steps))
@@ -352,11 +385,12 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # events on the stream the kernels run on
 
-    t = torch.tensor([wall, t_sc if args.shard == "band" else 0.0], dtype=torch.float64,
+    t = torch.tensor([wall, t_sc if args.shard == "band" else 0.0, kern_ms], dtype=torch.float64,
                      device="cpu" if backend == "gloo" else dev)
     if dist:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # timing bookkeeping only, not the data path
-    wall_max, scatter_max = float(t[0].item()), float(t[1].item())
+    # the slowest rank's wall time and the slowest rank's kernel time
+    wall_max, scatter_max, kern_ms = float(t[0].item()), float(t[1].item()), float(t[2].item())
 
     if args.shard == "band":
         # gather the bands to rank 0 (IPC handle + device copy), timed on its own
@@ -364,10 +398,11 @@ def main():
         if dist:
             dist.barrier()
         t_g = time.perf_counter()
+        last = bands_out[(nstep[0] - 1) % rot]  # the band of the last timed step
         if dist:
-            be.gather_distributed(shards, band, rank, world, dist)
+            be.gather_distributed(shards, last, rank, world, dist)
         else:
-            be.gather(mine, band)
+            be.gather(mine, last)
         be.sync()
         if dist:
             dist.barrier()
@@ -396,6 +431,39 @@ def main():
     if rank == 0 and world == 1 and args.shard == "image" and not args.no_probe:
         probe = reuse_probe(step_batch, rot, dev)
         log("reuse probe: %s" % json.dumps(probe))
+
+    alt = None
+    alt_frames = args.alt_frames if args.alt_frames >= 0 else (256 if args.config == "c2" else 0)
+    if args.shard == "image" and alt_frames and alt_frames != frames:
+        del src, dst
+        torch.cuda.empty_cache()
+
+        def make_alt(n):
+            rot_a = max(2, int(-(-2.5e9 // (n * (sw * sh + dw * dh)))))
+            g2 = torch.Generator(device=dev)
+            g2.manual_seed(4321 + rank)
+            sa = torch.randint(0, 256, (rot_a, n, sh, sw), dtype=torch.uint8, device=dev, generator=g2)
+            da = torch.empty((rot_a, n, dh, dw), dtype=torch.uint8, device=dev)
+            k = [0]
+
+            def st():
+                b = k[0] % rot_a
+                k[0] += 1
+                r.resize_device(n, sw, sw * sh, sa[b].data_ptr(), dw, dw * dh, da[b].data_ptr(), sp)
+
+            def cleanup():
+                # bit-exact spot check of the alt batch too (frames 0, mid, last of batch 0)
+                if rank == 0 and not args.no_verify:
+                    sys.path.insert(0, os.path.join(ROOT, "tests"))
+                    import oracle_lib as ol
+                    for f in sorted({0, n // 2, n - 1}):
+                        exp = ol.run_oracle(m, d, sw, sh, dw, dh, px, sa[0, f].cpu().numpy())
+                        if not bool((da[0, f].cpu().numpy() == exp).all()):
+                            raise SystemExit("alt batch MISMATCH at frame %d" % f)
+            return st, cleanup
+
+        alt = alt_batch(make_alt, alt_frames, sw * sh + dw * dh, dev)
+        log("alt batch: %s" % json.dumps(alt))
 
     cpu = None
     ref_bench = None
@@ -447,6 +515,9 @@ def main():
         }
         if band_info:
             res["band"] = band_info
+        if alt:
+            res["config"]["frames_per_gpu_alt"] = alt["frames"]
+            res["batch_alt"] = alt
         if probe:
             res["reuse_probe"] = probe
         if ref_bench:

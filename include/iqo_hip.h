@@ -56,11 +56,13 @@ enum {
     IQO_KERNEL_LINEAR_UP2 = 3,  /* exact 2x bilinear upsampling */
     IQO_KERNEL_TILE = 4,        /* general ratios, any layout: separable tiles (TH rows x CT columns) */
     IQO_KERNEL_WALK = 5,        /* general ratios, 4-byte aligned sources: wave walker, per-wave LDS ring */
-    IQO_KERNEL_LANCZOS_UP2 = 6, /* exact 2x Lanczos-2/3 upscale: register-window streamer + walker borders */
+    IQO_KERNEL_LANCZOS_UP2 = 6, /* exact 2x Lanczos-2/3 upscale: register-window streamer, every row and column in-kernel */
     IQO_KERNEL_LANCZOS_D32 = 7, /* exact 3:2 Lanczos-3 downscale: register-window streamer, borders in-kernel */
     IQO_KERNEL_AREA_D32 = 8,    /* exact 3:2 Area downscale: one wave per strip, no window */
     IQO_KERNEL_LANCZOS_U23 = 9, /* exact 2:3 Lanczos-3 upscale: register-window streamer, borders in-kernel */
-    IQO_KERNEL_LINEAR_U23 = 10  /* exact 2:3 Linear upscale: clamped halo, no border code */
+    IQO_KERNEL_LINEAR_U23 = 10, /* exact 2:3 Linear upscale: clamped halo, no border code */
+    IQO_KERNEL_LANCZOS_D31 = 11, /* exact 3:1 Lanczos-2/3 downscale: register window, symmetric taps, borders in-kernel */
+    IQO_KERNEL_RYX = 12          /* exact vertical ratio (9:4), tabled columns: register window + LDS work row */
 };
 
 typedef struct iqo_hip_plan iqo_hip_plan;
@@ -154,8 +156,10 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *plan, size_t srcStY, const uint8_t *
  * Copies nFrames blocks of bytesPerFrame bytes: block f from src + f*srcFrameSt to
  * dst + f*dstFrameSt.  A device < 0 means host memory.  Device to device on different GPUs:
  * hipMemcpyPeerAsync over xGMI when peer access is available, else staged through pinned host
- * memory (synchronous).  Asynchronous on `stream` (of the destination device, or of the source
- * device for device -> host) otherwise.  *path (may be NULL) reports the route: 0 same device,
+ * memory.  Ordering: every route is ordered after the work already queued on `stream` (of the
+ * destination device, or of the source device for device -> host).  The stream-ordered routes
+ * (0, 1, 3) are asynchronous on `stream`; the host-staging route (2) first waits for `stream` and
+ * the source device, then copies synchronously and has landed when the call returns.  *path (may be NULL) reports the route: 0 same device,
  * 1 peer DMA, 2 host staging, 3 host <-> device. */
 int iqo_hip_copy_frames(void *dst, int dstDevice, size_t dstFrameSt, const void *src, int srcDevice,
                         size_t srcFrameSt, size_t bytesPerFrame, size_t nFrames, void *stream, int *path);
@@ -188,7 +192,7 @@ int iqo_host_band_src_rows(int method, unsigned degree, size_t srcW, size_t srcH
 int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                         size_t pxScale);
 
-/* Drop-in classes (include/libiqo/*Resizer.hpp): how many objects this process constructed on the
+/* Drop-in classes (iqo::LanczosResizer, AreaResizer, LinearResizer): how many objects this process constructed on the
  * HIP backend and on the CPU backend (no gfx950 device; IQO_REQUIRE_HIP=1 forbids it). */
 void iqo_dropin_backend_counts(int *hip, int *cpu);
 

@@ -41,6 +41,9 @@ struct iqo_hip_plan {
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
+    int sweep = 1;          // block-shared streamer: persistent XCD sweep, nontemporal streams (speed only)
+    int sweepWg = 0;        // sweep: workgroups per CU (0 = all resident)
+    int symbNt = 0;         // block-shared streamer, grid layout: nontemporal streams (A/B)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
@@ -56,12 +59,18 @@ struct iqo_hip_plan {
     // general-ratio wave walker (plan.hpp WalkTables; option "walk" = 0 keeps tile_kernel)
     iqo_amd::WalkTables wt;
     bool useWalk = true;
-    // exact 2x Lanczos upscale kernel on the main rows x middle columns (option "up2" = 0: walker only)
+    // exact 2x Lanczos upscale kernel, every row and column in-kernel (option "up2" = 0: walker only)
     iqo_amd::Up2Tables ut;
     bool useUp2 = true;
     // exact 3:2 Lanczos-3 downscale kernel on the main rows (option "d32" = 0: walker only)
     iqo_amd::D32Tables dt;
+    iqo_amd::D31Tables t31;
+    iqo_amd::RyxTables ryx;
+    uint32_t *dRyxRowCoef = nullptr, *dRyxColCoef = nullptr;
+    int4 *dRyxCols = nullptr;
     bool useD32 = true;
+    bool useD31 = true;
+    bool useRyx = true;
     // exact 2:3 Linear upscale kernel (option "l23" = 0: walker only)
     iqo_amd::L23Tables lt;
     bool useL23 = true;
@@ -308,6 +317,9 @@ void free_plan(iqo_hip_plan *h)
     (void)hipFree(h->dTRowTap);
     (void)hipFree(h->dTColCoef);
     (void)hipFree(h->dTColA);
+    (void)hipFree(h->dRyxRowCoef);
+    (void)hipFree(h->dRyxColCoef);
+    (void)hipFree(h->dRyxCols);
     (void)hipFree(h->dWSpans);
     (void)hipFree(h->dWRowTap);
     (void)hipFree(h->dWRows);
@@ -384,6 +396,20 @@ int upload_tile(iqo_hip_plan *h)
     // exact-ratio kernels (no device tables: their coefficients are kernel arguments)
     iqo_amd::build_up2(h->p, h->wt, &h->ut);
     iqo_amd::build_d32(h->p, h->wt, &h->dt);
+    iqo_amd::build_d31(h->p, &h->t31);
+    iqo_amd::build_ryx(h->p, &h->ryx);
+    if (h->ryx.ok) {
+        std::vector<int4> rc(h->ryx.cols.size() / 4);
+        for (size_t i = 0; i < rc.size(); ++i)
+            rc[i] = make_int4(h->ryx.cols[4 * i], h->ryx.cols[4 * i + 1], h->ryx.cols[4 * i + 2], 0);
+        int rc2 = upload(&h->dRyxRowCoef, h->ryx.rowCoef.data(), h->ryx.rowCoef.size());
+        if (!rc2)
+            rc2 = upload(&h->dRyxColCoef, h->ryx.colCoef.data(), h->ryx.colCoef.size());
+        if (!rc2)
+            rc2 = upload(&h->dRyxCols, rc.data(), rc.size());
+        if (rc2)
+            return rc2;
+    }
     iqo_amd::build_a32(h->p, &h->at);
     iqo_amd::build_u23(h->p, &h->vt);
     iqo_amd::build_l23(h->p, &h->lt);
@@ -504,6 +530,9 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
         l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
     l.np = h->lanes;
     l.xcd = h->xcdOrder;
+    l.sweep = h->sweep;
+    l.sweepWg = h->sweepWg;
+    l.nt = h->symbNt;
     return l;
 }
 
@@ -517,8 +546,8 @@ iqo_amd::AreaDev area_dev(const iqo_hip_plan *h)
     a.dstW = p.dstW;
     for (int i = 0; i < a.KY; ++i)
         a.cy[i] = pair16(p.far.cy[i], p.far.cy[i]);
-    for (int i = 0; i < a.KX / 2; ++i)
-        a.cx[i] = pair16(p.far.cx[2 * i], p.far.cx[2 * i + 1]);
+    for (int i = 0; i < (a.KX + 1) / 2; ++i)  // odd KX: the last pair is (c_{KX-1}, 0)
+        a.cx[i] = pair16(p.far.cx[2 * i], 2 * i + 1 < a.KX ? p.far.cx[2 * i + 1] : 0);
     a.dstH = p.dstH;
     return a;
 }
@@ -629,6 +658,53 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     return d;
 }
 
+iqo_amd::D31Dev d31_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::D31Tables &t = h->t31;
+    iqo_amd::D31Dev d;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.np = h->lanes;
+    d.pd = h->ratioPrefetch;
+    d.variant = t.variant;
+    d.cc = t.cc;
+    std::memcpy(d.cp, t.cp, sizeof d.cp);
+    std::memcpy(d.cxe, t.cxe, sizeof d.cxe);
+    std::memcpy(d.cxo, t.cxo, sizeof d.cxo);
+    std::memcpy(d.xM, t.xM, sizeof d.xM);
+    std::memcpy(d.xT, t.xT, sizeof d.xT);
+    d.m0 = t.m0;
+    d.m1 = t.m1;
+    std::memcpy(d.yM, t.yM, sizeof d.yM);
+    std::memcpy(d.yS, t.yS, sizeof d.yS);
+    return d;
+}
+
+iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::RyxTables &t = h->ryx;
+    iqo_amd::RyxDev d;
+    d.lanczos = h->p.method == iqo_amd::kLanczos;
+    d.srcW = h->p.srcW;
+    d.srcH = h->p.srcH;
+    d.dstW = h->p.dstW;
+    d.dstH = h->p.dstH;
+    d.P = t.P;
+    d.Q = t.Q;
+    d.taps = t.taps;
+    d.NP = t.NP;
+    d.m0 = t.m0;
+    d.m1 = t.m1;
+    std::memcpy(d.yM, t.yM, sizeof d.yM);
+    std::memcpy(d.yS, t.yS, sizeof d.yS);
+    d.rowCoef = h->dRyxRowCoef;
+    d.cols = h->dRyxCols;
+    d.colCoef = h->dRyxColCoef;
+    return d;
+}
+
 iqo_amd::L23Dev l23_dev(const iqo_hip_plan *h)
 {
     iqo_amd::L23Dev d;
@@ -712,6 +788,10 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_LANCZOS_UP2;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->dt.ok && h->useD32)
         k = IQO_KERNEL_LANCZOS_D32;
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->t31.ok && h->useD31)
+        k = IQO_KERNEL_LANCZOS_D31;
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->ryx.ok && h->useRyx)
+        k = IQO_KERNEL_RYX;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->at.ok && h->useA32)
         k = IQO_KERNEL_AREA_D32;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->vt.ok && h->useU23)
@@ -730,8 +810,12 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     int kernel = h->forceGeneral ? IQO_KERNEL_GENERAL : p.kernel;
     if (kernel == IQO_KERNEL_LANCZOS_STREAM && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.flz.KX, dstSt, dstFrameSt)))
         kernel = IQO_KERNEL_GENERAL;
-    if (kernel == IQO_KERNEL_AREA_INT && !(aligned(src, 16, srcSt, srcFrameSt) && aligned(dst, 16 / p.far.KX, dstSt, dstFrameSt)))
-        kernel = IQO_KERNEL_GENERAL;
+    if (kernel == IQO_KERNEL_AREA_INT) {
+        // 16-B loads / 16 / KX output bytes per thread; 12-B loads / 12 / KX bytes when KX is 3 or 6
+        const int cols = 16 % p.far.KX == 0 ? 16 : 12;
+        if (!(aligned(src, cols == 16 ? 16 : 4, srcSt, srcFrameSt) && aligned(dst, cols / p.far.KX, dstSt, dstFrameSt)))
+            kernel = IQO_KERNEL_GENERAL;
+    }
     if (kernel == IQO_KERNEL_LINEAR_UP2 && !(aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 16, dstSt, dstFrameSt)))
         kernel = IQO_KERNEL_GENERAL;
     if (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral && h->tt.ok && h->useTile)
@@ -748,6 +832,14 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->dt.ok && h->useD32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_D32;
+    // the 3:1 Lanczos kernel loads 12 B per lane (4-byte aligned) and stores 4 B per lane
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->t31.ok && h->useD31 &&
+        aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_LANCZOS_D31;
+    // exact vertical ratio, tabled columns: dword loads, 2-byte stores
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->ryx.ok && h->useRyx &&
+        aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 2, dstSt, dstFrameSt))
+        kernel = IQO_KERNEL_RYX;
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_AREA_D32;
@@ -811,6 +903,22 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
         const size_t n = (nFrames + chunk - 1) / chunk;  // equal launches, not one straggler
         chunk = (nFrames + n - 1) / n;
     }
+    // the exact-ratio kernels instantiate a few prefetch depths each; any other forced depth is an
+    // error, not a silent fall-back to the default kernel
+    if (h->ratioPrefetch > 0) {
+        const int pd = h->ratioPrefetch;
+        bool ok = true;
+        if (kernel == IQO_KERNEL_LANCZOS_D32)
+            ok = h->dt.variant == 0 ? (pd == 1 || pd == 2 || pd == 4) : (pd == 1 || pd == 3);
+        else if (kernel == IQO_KERNEL_LANCZOS_D31)
+            ok = h->t31.variant == 0 ? (pd == 1 || pd == 5) : (pd == 1 || pd == 2 || pd == 4);
+        else if (kernel == IQO_KERNEL_LANCZOS_U23 || kernel == IQO_KERNEL_LINEAR_U23)
+            ok = pd == 1 || pd == 2;
+        else if (kernel == IQO_KERNEL_AREA_D32)
+            ok = pd == 2 || pd == 4 || pd == 8;
+        if (!ok)
+            return IQO_HIP_EINVAL;
+    }
     for (size_t f0 = 0; f0 < nFrames; f0 += chunk) {
         const iqo_amd::Io io = make_io(std::min(chunk, nFrames - f0), src + f0 * srcFrameSt, srcSt, srcFrameSt, srcRow0,
                                        s1, dst + f0 * dstFrameSt, dstSt, dstFrameSt, rb);
@@ -829,6 +937,10 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_up2(up2_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_LANCZOS_D32)
             e = iqo_amd::launch_d32(d32_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_LANCZOS_D31)
+            e = iqo_amd::launch_d31(d31_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_RYX)
+            e = iqo_amd::launch_ryx(ryx_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_AREA_D32)
             e = iqo_amd::launch_a32(a32_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_LANCZOS_U23)
@@ -925,6 +1037,20 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->ringPack = value != 0;
         return IQO_HIP_OK;
     }
+    if (!std::strcmp(key, "sweep")) {  // block-shared Lanczos streamer: persistent XCD sweep (A/B)
+        h->sweep = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "symb_nt")) {  // block-shared streamer, grid layout: nontemporal streams (A/B)
+        h->symbNt = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "sweep_wg")) {  // sweep: workgroups per CU (0 = all resident)
+        if (value < 0 || value > 8)
+            return IQO_HIP_EINVAL;
+        h->sweepWg = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
     if (!std::strcmp(key, "xcd_order")) {  // block-shared Lanczos streamer workgroup order (A/B)
         h->xcdOrder = value != 0;
         return IQO_HIP_OK;
@@ -986,10 +1112,20 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->useA32 = value != 0;
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "ratio_prefetch")) {  // exact 3:2 kernels: row groups loaded ahead (speed only)
+    if (!std::strcmp(key, "ratio_prefetch")) {  // exact-ratio kernels: row groups loaded ahead (speed only);
+                                                 // a depth the plan's kernel does not instantiate fails the
+                                                 // resize call with IQO_HIP_EINVAL
         if (value < 0 || value > 8)
             return IQO_HIP_EINVAL;
         h->ratioPrefetch = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryx")) {  // 0: exact-vertical-ratio downscales use the general kernels
+        h->useRyx = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "d31")) {  // 0: exact 3:1 Lanczos downscales use the general kernels
+        h->useD31 = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "d32")) {  // 0: exact 3:2 Lanczos-3 downscales use the wave walker alone
@@ -1364,7 +1500,18 @@ int iqo_hip_copy_frames(void *dst, int dstDevice, size_t dstFrameSt, const void 
             *path = 1;
         return IQO_HIP_OK;
     }
-    // no peer path: stage through pinned host memory, block by block (synchronous)
+    // no peer path: stage through pinned host memory, block by block, synchronously.  The blocking
+    // hipMemcpy calls run on the devices' null streams, which a caller's non-blocking stream does
+    // not order against: first drain `stream` (work still writing src or reading dst) and the
+    // source device, so this route is ordered like the stream-ordered ones; when it returns the
+    // copy has landed (iqo_hip.h).
+    if (s && hipStreamSynchronize(s) != hipSuccess)
+        return IQO_HIP_EHIP;
+    {
+        DeviceGuard sg(srcDevice);
+        if (!sg.ok() || hipDeviceSynchronize() != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
     uint8_t *h = nullptr;
     if (hipHostMalloc(reinterpret_cast<void **>(&h), bytesPerFrame, hipHostMallocDefault) != hipSuccess)
         return IQO_HIP_ENOMEM;
@@ -1503,6 +1650,8 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     iqo_amd::build_walk_tables(h.p, h.tt, &h.wt);
     iqo_amd::build_up2(h.p, h.wt, &h.ut);
     iqo_amd::build_d32(h.p, h.wt, &h.dt);
+    iqo_amd::build_d31(h.p, &h.t31);
+    iqo_amd::build_ryx(h.p, &h.ryx);
     iqo_amd::build_a32(h.p, &h.at);
     iqo_amd::build_u23(h.p, &h.vt);
     iqo_amd::build_l23(h.p, &h.lt);

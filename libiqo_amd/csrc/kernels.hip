@@ -573,6 +573,9 @@ struct LanczosArgs {
     int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
     int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
     int lastLanes;           // block-shared streamer: lanes of the last DMA chunk (0 = all 64)
+    int sweep;               // block-shared streamer: persistent XCD sweep over (frame, band) items
+    int frames;              // items = frames x bands (sweep)
+    int noAlt;               // every band walks top-down (sweep: nontemporal streams prefer it)
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -840,23 +843,22 @@ __device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_
 // dma_row for the lanes of `mask` only (masked-off lanes write nothing to LDS): the last chunk of a
 // ring row DMAs just the bytes the row needs, so the ring rows can be packed tighter than 1 KiB
 __device__ __forceinline__ void dma_row_masked(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff,
-                                               uint64_t mask)
+                                               uint64_t mask, bool nt = IQO_DMA_NT)
 {
     uint32_t keep;
     uint64_t save;
-#if IQO_DMA_NT
-    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %3, %4, %5 offen nt lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
-                 : "=&s"(keep), "=&s"(save)
-                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
-                 : "memory");
-#else
-    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %3, %4, %5 offen lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
-                 : "=&s"(keep), "=&s"(save)
-                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
-                 : "memory");
-#endif
+    if (nt)
+        asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %3, %4, %5 offen nt lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+                     : "=&s"(keep), "=&s"(save)
+                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
+                     : "memory");
+    else
+        asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                     "buffer_load_dwordx4 %3, %4, %5 offen lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+                     : "=&s"(keep), "=&s"(save)
+                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
+                     : "memory");
 }
 
 template <int N>
@@ -1107,7 +1109,19 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 // row before it is refilled.  Waves with fewer chunks than CPW DMA into a sink so the vm-counter
 // pattern is the same in every wave.
 
-template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, bool NT = false>
+#ifndef IQO_SWEEP_NTL
+#define IQO_SWEEP_NTL 1  // sweep: nontemporal LDS-DMA source loads and window prologue loads
+#endif
+#ifndef IQO_SWEEP_NTS
+#define IQO_SWEEP_NTS 1  // sweep: nontemporal output stores
+#endif
+#ifndef IQO_SWEEP_ALT
+#define IQO_SWEEP_ALT 0  // sweep: odd bands walk bottom-up as in the grid layout
+#endif
+#ifndef IQO_SWEEP_EDGE_DEF
+#define IQO_SWEEP_EDGE_DEF 1  // nontemporal modes: the edge waves store with the default policy
+#endif
 #ifndef IQO_SYMB_WAVES_PER_EU
 #define IQO_SYMB_WAVES_PER_EU 4
 #endif
@@ -1185,7 +1199,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     // same time (both at their start or both at their end) and the second read hits the
     // Infinity Cache instead of HBM.  The window arithmetic is symmetric, so only the row order
     // changes: walk index t of iteration i is source row rowAt(i, t).
-    const int dir = ((band & 1) && !(dbg & 32)) ? -1 : 1;
+    const int dir = ((band & 1) && !(dbg & 32) && (!a.noAlt || IQO_SWEEP_ALT)) ? -1 : 1;
     const int rFirst = 2 * y0 + L.offY;                 // first source row the band reads
     const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;  // last source row the band reads
     const int nRows = y1 - y0;
@@ -1217,11 +1231,11 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             const uint32_t d0 = real ? s + 16 + 1024 * c : ldsBase + sinkLds;
             const uint32_t d1 = real ? d0 + rowPitch : d0;
             if (real && c == a.chunks - 1 && lastLanes < 64) {  // uniform
-                dma_row_masked(d0, v, srcR, row_soff(r), lastMask);
-                dma_row_masked(d1, v, srcR, row_soff(r + dir), lastMask);
+                dma_row_masked(d0, v, srcR, row_soff(r), lastMask, (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
+                dma_row_masked(d1, v, srcR, row_soff(r + dir), lastMask, (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
             } else {
-                dma_row(d0, v, srcR, row_soff(r));
-                dma_row(d1, v, srcR, row_soff(r + dir));
+                dma_row(d0, v, srcR, row_soff(r), (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
+                dma_row(d1, v, srcR, row_soff(r + dir), (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
             }
         }
     };
@@ -1277,7 +1291,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         uint4 w0[NY - 2];
 #pragma unroll
         for (int t = 0; t < NY - 2; ++t) {
-            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), IQO_SYMB_PRO_NT ? 2 : 0);
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), ((NT && IQO_SWEEP_NTL) || IQO_SYMB_PRO_NT) ? 2 : 0);
             w0[t] = make_uint4(q.x, q.y, q.z, q.w);
         }
 #pragma unroll
@@ -1432,7 +1446,13 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{o.x, o.y, o.x, o.y}, dstR, st16, (yy - a.io.dstRow0) * dstSt, 0);
         } else
 #endif
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, IQO_SYMB_NT_STORE ? 2 : 0);
+        // nontemporal stores leave L2 at once; the edge waves' lines get their border bytes rewritten
+        // up to EB rows later (flush_edges), so those waves keep the default policy and the two
+        // writes of a line merge in L2 instead of reaching HBM as two partial-line writes
+        if ((NT && IQO_SWEEP_NTS && !(IQO_SWEEP_EDGE_DEF && (edgeL || edgeR))) || IQO_SYMB_NT_STORE)
+            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 2);
+        else
+            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every 64 rows and at the band end one pass divides them, one row per lane
@@ -1452,9 +1472,37 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
-template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, int MODE = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WAVES_PER_EU))) void lanczos_symb_kernel(LanczosArgs a)
 {
+    // MODE 2 is the sweep layout (nontemporal), MODE 0 / 1 the (band, frame) grid with default /
+    // nontemporal streams (prep_lanczos picks the instantiation): one body per instantiation
+    constexpr bool NT = MODE >= 1;
+    if constexpr (MODE == 2) {
+        // Persistent XCD sweep (option "sweep", default for large batches): the (frame, band) items
+        // in frame-major order are cut into 8 contiguous ranges, XCD x (workgroups b with b mod 8 = x
+        // under the round-robin placement; speed only) takes range x, and its workgroups take the
+        // items j, j + G/8, ... of it.  At any time an XCD reads a compact window of its own frames
+        // (one band per workgroup, bands of ~34 rows), and loads and stores are nontemporal: on fresh
+        // data this memory stream sustains ~6.0-6.3 TB/s against 5.2-5.4 for one workgroup per band
+        // scattered over the batch (scripts/ubench/c2mem.hip, profiles/r03/ubench_c2mem_*.txt).
+        const unsigned G = gridDim.x, n = static_cast<unsigned>(a.bands) * static_cast<unsigned>(a.frames);
+        unsigned lo = 0, hi = n, j = blockIdx.x, step = G;
+        if (G % 8u == 0) {
+            const unsigned x = blockIdx.x & 7u, q = n >> 3, r = n & 7u;
+            lo = x * q + min(x, r);
+            hi = lo + q + (x < r ? 1u : 0u);
+            j = blockIdx.x >> 3;
+            step = G >> 3;
+        }
+        for (unsigned i = lo + j; i < hi; i += step) {
+            const unsigned frame = i / static_cast<unsigned>(a.bands);
+            lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE, NT>(a, i - frame * static_cast<unsigned>(a.bands), frame);
+            // every wave's reads of the ring and edge slots are done before the next item's DMAs
+            __syncthreads();
+        }
+        return;
+    } else {
     unsigned bx = blockIdx.x, by = blockIdx.y;
     if (a.xcd) {
         // XCD-aware order (speed only): the band workgroups of one frame go to one XCD, so the
@@ -1465,7 +1513,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WA
         by = lg / bands;
         bx = lg - by * bands;
     }
-    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, bx, by);
+    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE, NT>(a, bx, by);
+    }
 }
 
 
@@ -1802,7 +1851,11 @@ struct AreaArgs {
 template <int KX, int KYT>
 __device__ __forceinline__ void area_int_kernel_body(const AreaArgs &a, const unsigned bx, const unsigned by)
 {
-    constexpr int OUTS = 16 / KX;
+    // a thread owns COLS source columns: 16 (one 16-B load per row) when KX divides 16, else 12
+    // (one 12-B load; KX = 3, 6)
+    constexpr int COLS = 16 % KX == 0 ? 16 : 12;
+    constexpr int OUTS = COLS / KX;
+    static_assert(COLS % KX == 0, "whole outputs per thread");
     const int KY = KYT ? KYT : a.g.KY;
     const int64_t gid = static_cast<int64_t>(bx) * blockDim.x + threadIdx.x;
     const int64_t total = static_cast<int64_t>(a.rowEnd - a.rowBegin) * a.groups;
@@ -1811,24 +1864,45 @@ __device__ __forceinline__ void area_int_kernel_body(const AreaArgs &a, const un
     const int y = a.rowBegin + static_cast<int>(gid / a.groups);
     const int gcol = static_cast<int>(gid % a.groups);
     const uint8_t *s = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt +
-                       static_cast<int64_t>(KY * y - a.io.srcRow0) * a.io.srcSt + 16 * gcol;
-    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                       static_cast<int64_t>(KY * y - a.io.srcRow0) * a.io.srcSt + COLS * gcol;
+    uint32_t acc[COLS / 2] = {};
 #pragma unroll 4
     for (int i = 0; i < KY; ++i) {
-        uint4 v = load16_nt(s + static_cast<int64_t>(i) * a.io.srcSt);
-        uint32_t w[8];
-        unpack16(v, w);
+        uint32_t w[COLS / 2];
+        if constexpr (COLS == 16) {
+            unpack16(load16_nt(s + static_cast<int64_t>(i) * a.io.srcSt), w);
+        } else {
+            const u32x3 v = __builtin_nontemporal_load(reinterpret_cast<const u32x3 *>(s + static_cast<int64_t>(i) * a.io.srcSt));
+            unpack4(v.x, w[0], w[1]);
+            unpack4(v.y, w[2], w[3]);
+            unpack4(v.z, w[4], w[5]);
+        }
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
+        for (int c = 0; c < COLS / 2; ++c)
             acc[c] = pk_mad(w[c], a.g.cy[i], acc[c]);
     }
     uint32_t out[OUTS];
 #pragma unroll
     for (int k = 0; k < OUTS; ++k) {
         uint32_t sum = 1u << 22;
+        if constexpr (KX % 2 == 0) {
 #pragma unroll
-        for (int p = 0; p < KX / 2; ++p)
-            sum = udot2(acc[(KX * k) / 2 + p], a.g.cx[p], sum);
+            for (int p = 0; p < KX / 2; ++p)
+                sum = udot2(acc[(KX * k) / 2 + p], a.g.cx[p], sum);
+        } else {
+            // odd KX (3): output k's window starts on column 3k; even starts take the aligned pairs
+            // (c0, c1), (c2, 0); odd starts the odd-aligned pair (c0, c1) by alignbit, then the
+            // pair holding column 3k + 2 in its high half with (0, c2)
+            static_assert(KX == 3, "odd ratios: 3");
+            const int c0 = 3 * k;
+            if (c0 % 2 == 0) {
+                sum = udot2(acc[c0 / 2], a.g.cx[0], sum);
+                sum = udot2(acc[c0 / 2 + 1], a.g.cx[1], sum);
+            } else {
+                sum = udot2(__builtin_amdgcn_alignbit(acc[(c0 + 1) / 2], acc[(c0 - 1) / 2], 16), a.g.cx[0], sum);
+                sum = udot2(acc[(c0 + 1) / 2], a.g.cx[1] << 16, sum);
+            }
+        }
         int v = static_cast<int16_t>(static_cast<int>(sum) >> 23);
         uint16_t u = static_cast<uint16_t>(v);
         out[k] = opaque(u > 255 ? 255u : u);
@@ -2517,6 +2591,418 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
             emit(W, y + 1, 2 * v + 1);
         });
         flush(2 * (kLo + base));
+    }
+}
+
+// ================================================================ exact 3:1 Lanczos-2/3 downscale
+//
+// Lanczos-3 (Lanczos-2) at exactly 1/3 (e.g. 3840x2160 -> 1280x720, 1920x1080 -> 640x360;
+// plan.cpp build_d31).  The reference's tables for this ratio have one phase: 18 (12) taps,
+// window start 3y - 8 (3y - 5), tap 0 zero and taps 1.. symmetric about the centre
+// (IQOLanczosResizerImpl_Generic.cpp:144-190 tables, :404-454 row loop, :582-612 columns).  One WAVE
+// per (row band, output strip, frame) walks the band's rows top to bottom, no barrier:
+//
+// * lane l (1..np) owns output columns [x0 + 4(l-1), +4) and source columns [cb, cb + 12),
+//   cb = 3 x0 - 12 + 12 l; lanes 0 and np+1 are the halo.  Each source row is loaded once per band
+//   (12 B per lane, PD output rows ahead, branch-free so the compiler's vm waits are exact) and
+//   widened to six u16 pairs in a register window of NW rows (static names: U = NW / 3 output rows
+//   per trip, each adding 3 source rows).
+// * Vertical: the symmetric taps pair up -- the window's centre row times its coefficient plus
+//   NPY pair sums (s[CEN - d] + s[CEN + d], <= 510 per u16 half, one full-rate v_add_u32 for both
+//   halves) times theirs, packed MACs whose low 16 bits are the reference's int16 wrap.
+// * Horizontal: work columns cb + EB .. cb + EB + 2 NE - 1 as u16 pairs E[e] (the outer ones from
+//   the neighbouring lanes by DPP); output j's window starts at cb + XS + 3j: an even start takes
+//   the pairs from its start with coefficient pairs (c0, c1), (c2, c3), ..; an odd start skips
+//   tap 0 (zero in these tables) and takes the pairs from start + 1 with (c1, c2), (c3, c4), .. --
+//   every pair aligned, no v_alignbit.
+// * Borders as lanczos_d32_kernel: source rows / columns outside the image load as zero, so the
+//   sums are the reference's masked numerators (:464-490, :539-574); masked border rows divide their
+//   work pairs (int16(n * 64 / deno), magic_y); the <= 4 border columns per side lie in the edge
+//   lane, which parks its 4 raw sums in LDS, and once per trip lanes 0..U-1 rewrite one row's 4
+//   edge bytes each with the exact division.
+struct D31Args {
+    D31Dev d;
+    Io io;
+    int rowBegin, rowEnd, rowsPerBand, bands, wavesPerRow, np;
+    int srcBytes, dstBytes;
+    unsigned nWaves;
+};
+
+// tap structure per variant: window rows NR (start 3y + YA), centre row CEN, pair distances, work
+// pairs E (first column EB, count NE, NL from each neighbour), column window start XS (tap 0), and
+// coefficient pairs per output NPX
+template <int VAR>
+struct D31Shape;
+template <>
+struct D31Shape<0> {  // Lanczos-3: 18 taps, non-zero taps 2..16, centre 9
+    static constexpr int NR = 15, YA = -6, CEN = 7, NPY = 5;
+    static constexpr int DIST[5] = {1, 2, 4, 5, 7};
+    static constexpr int EB = -8, NE = 14, NL = 4, XS = -8, NPX = 9;
+};
+template <>
+struct D31Shape<1> {  // Lanczos-2: 12 taps, non-zero taps 1..11, centre 6
+    static constexpr int NR = 11, YA = -4, CEN = 5, NPY = 4;
+    static constexpr int DIST[5] = {1, 2, 4, 5, 0};
+    static constexpr int EB = -4, NE = 10, NL = 2, XS = -5, NPX = 6;
+};
+
+template <int PD, int VAR>
+__global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
+{
+    using S = D31Shape<VAR>;
+    constexpr int NW = (S::NR + 2) / 3 * 3;  // register window rows (whole groups of 3)
+    constexpr int U = NW / 3;                // output rows per unrolled trip (window slots repeat)
+    constexpr int OOB = 0x7ff00000;
+    constexpr int OWN = -S::EB / 2;          // E index of the lane's own pair 0
+    static_assert(U % PD == 0, "prefetch slots repeat within a trip");
+    static_assert(OWN - S::NL >= 0 && OWN + 6 + S::NL == S::NE, "work pairs: NL from each neighbour");
+    const D31Dev &d = a.d;
+    __shared__ int4 park[4][2][8];  // per wave, side, row slot: the edge lane's 4 raw sums
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    if (gw >= a.nWaves)
+        return;  // whole wave; no barrier in this kernel
+    const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
+    const unsigned rest = gw / static_cast<unsigned>(a.wavesPerRow);
+    const int band = static_cast<int>(rest % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(rest / static_cast<unsigned>(a.bands));
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;
+    const int nR = y1 - y0;
+
+    const int opw = 4 * a.np;
+    const int x0 = max(0, min(wcol * opw, d.dstW - opw));
+    const int cb = 3 * x0 - 12 + 12 * lane;
+    const bool produce = lane >= 1 && lane <= a.np;
+    const int voff = (lane <= a.np + 1 && cb >= 0 && cb + 12 <= d.srcW) ? cb : OOB;
+    const int stoff = produce ? x0 + 4 * (lane - 1) : OOB;
+    const bool edgeL = x0 == 0, edgeR = x0 + opw >= d.dstW;  // wave holds border columns (uniform)
+    const bool laneL = edgeL && lane == 1, laneR = edgeR && lane == a.np;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+
+    // relative row q = source row rBase + q (output y0 + v reads relative rows 3v .. 3v + NR - 1);
+    // rows outside the image read as zero (the masked border sums), rows past the band's last
+    // output are not loaded, rows outside the call's window are clamped (never used)
+    const int rBase = 3 * y0 + S::YA;
+    const int rLast = 3 * (y1 - 1) + S::YA + S::NR - 1;
+    const int srcLast = a.io.srcRowEnd - 1;
+    auto load_row = [&](int q) -> u32x3 {
+        const int r = rBase + q;
+        const int rc = min(max(r, srcRow0), srcLast);
+        const bool in = r >= 0 && r < d.srcH && r <= rLast;
+        return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
+        P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
+        P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
+        P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
+        P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);
+        P[4] = __builtin_amdgcn_perm(0u, v.z, 0x0c010c00u);
+        P[5] = __builtin_amdgcn_perm(0u, v.z, 0x0c030c02u);  // (cb+10, cb+11)
+    };
+    auto store_row = [&](uint32_t o, int voffs, int y, bool ok) {
+        __builtin_amdgcn_raw_buffer_store_b32(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+    };
+    // horizontal pass of one output row from the lane's six work pairs; the edge lane parks its sums
+    auto emit = [&](const uint32_t (&W)[6], int y, int slot) {
+        uint32_t E[S::NE];
+#pragma unroll
+        for (int e = 0; e < S::NL; ++e)
+            E[e] = static_cast<uint32_t>(
+                __builtin_amdgcn_mov_dpp(static_cast<int>(W[6 - S::NL + e]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+            E[OWN + e] = W[e];
+#pragma unroll
+        for (int e = 0; e < S::NL; ++e)
+            E[OWN + 6 + e] = static_cast<uint32_t>(
+                __builtin_amdgcn_mov_dpp(static_cast<int>(W[e]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        int sum[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int st = S::XS + 3 * j;           // window start (tap 0) relative to cb
+            const bool odd = (st & 1) != 0;
+            const int e0 = ((odd ? st + 1 : st) - S::EB) / 2;
+            int acc = 1 << 19;
+#pragma unroll
+            for (int q = 0; q < S::NPX; ++q)
+                acc = sdot2(E[e0 + q], odd ? d.cxo[q] : d.cxe[q], acc);
+            sum[j] = acc;
+        }
+        store_row(pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]), stoff, y, y >= y0 && y < y1);
+        if (edgeL || edgeR) {  // uniform
+            if (laneL || laneR)
+                park[wib][laneL ? 0 : 1][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+        }
+    };
+    // once per trip: lane r < U rewrites the 4 edge bytes of row yt + r from the parked sums
+    auto flush = [&](int yt) {
+        uint32_t oL = 0u, oR = 0u;
+        if (edgeL || edgeR) {  // uniform
+            __builtin_amdgcn_wave_barrier();
+            auto fix = [&](int side) {
+                const int4 p = park[wib][side][lane & 7];
+                const int sv[4] = {p.x, p.y, p.z, p.w};
+                uint32_t b[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    b[j] = min(__umulhi(static_cast<uint32_t>(max(sv[j], 0)), d.xM[side][j]) >> d.xT[side][j], 255u);
+                return b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+            };
+            if (edgeL)
+                oL = fix(0);
+            if (edgeR)
+                oR = fix(1);
+        }
+        const int y = yt + lane;
+        const bool ok = lane < U && y >= y0 && y < y1;
+        store_row(oL, edgeL ? 0 : OOB, y, ok);
+        store_row(oR, edgeR ? d.dstW - 4 : OOB, y, ok);
+    };
+    // masked border row (uniform, rare): work = int16(n * 64 / deno)
+    auto border_row = [&](uint32_t (&W)[6], int y) {
+        if (y < d.m0 || y >= d.m1) {
+            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
+            const uint32_t m = d.yM[side][i];
+            const int sh = d.yS[side][i];
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = ydiv2(W[c], m, sh);
+        }
+    };
+
+    uint32_t R[NW][6];
+    // the window of output y0 without its newest 3 rows: relative rows 0 .. NW-4 -> slots 0 .. NW-4
+#pragma unroll
+    for (int q = 0; q < NW - 3; ++q)
+        widen(load_row(q), R[q]);
+    // prefetch: output y0 + v adds relative rows 3v + NW-3 .. 3v + NW-1 (slots mod NW)
+    u32x3 pre[PD][3];
+#pragma unroll
+    for (int v = 0; v < PD; ++v) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            pre[v][i] = load_row(3 * v + NW - 3 + i);
+        // the loop's store pattern (one row per step), dropped, so the header waits are steady-state
+        __builtin_amdgcn_raw_buffer_store_b32(0u, dstR, OOB, 0, 0);
+    }
+    // and the trip's two flush stores
+    __builtin_amdgcn_raw_buffer_store_b32(0u, dstR, OOB, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(0u, dstR, OOB, 0, 0);
+    for (int base = 0; base < nR; base += U) {
+        static_for<U>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int g = base + v;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                widen(pre[v % PD][i], R[(3 * v + NW - 3 + i) % NW]);
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                pre[v % PD][i] = load_row(3 * (g + PD) + NW - 3 + i);
+            // window row w of this output is slot (3v + w) mod NW
+            uint32_t W[6];
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                W[c] = pk_mul(R[(3 * v + S::CEN) % NW][c], d.cc);
+#pragma unroll
+            for (int k = 0; k < S::NPY; ++k)
+#pragma unroll
+                for (int c = 0; c < 6; ++c)
+                    W[c] = pk_mad(R[(3 * v + S::CEN - S::DIST[k]) % NW][c] + R[(3 * v + S::CEN + S::DIST[k]) % NW][c],
+                                  d.cp[k], W[c]);
+            border_row(W, y0 + g);
+            emit(W, y0 + g, v);
+        });
+        flush(y0 + base);
+    }
+}
+
+// ================================================================ exact vertical ratio, any horizontal ratio
+//
+// Downscales whose rows follow an exact ratio P:Q but whose columns do not (1920x1080 -> 854x480:
+// rows 9:4, columns 960:427, 427 column phases).  plan.cpp build_ryx.  One WORKGROUP (8 waves) per
+// (row band, frame), the whole width:
+//
+// * Vertical: thread t owns source columns [4t, 4t + 4) (one dword per row) and walks the band's
+//   rows with a register window of NW source rows widened to u16 pairs (static names: U groups of Q
+//   output rows per trip, each group adding P rows, loaded one group ahead).  Output y = Q m + j
+//   takes phase j's taps from window row floor(P j / Q) (IQOLanczosResizerImpl_Generic.cpp:404-454
+//   / IQOAreaResizerImpl_Generic.cpp:271-293 row loops): packed MACs, 16-bit wrap; masked Lanczos
+//   border rows (rows outside the image load as zero) are divided in place (:464-490).
+// * The work row goes to LDS (u16, zero padding either side, double-buffered: one barrier per row).
+// * Horizontal: thread t computes output columns 2t, 2t + 1 from the table: NP coefficient pairs in
+//   VGPRs for the whole band, NP dword reads from the work row at the column's even window start,
+//   v_dot2 (:582-612 / :340-368); Lanczos columns end in an exact multiply-high division (the
+//   identity 2^20 in the interior, the border divisor of :539-574 at the edges).
+struct RyxArgs {
+    RyxDev d;
+    Io io;
+    int rowBegin, rowEnd, groupBegin, rowsPerBand, bands;
+    int srcBytes, dstBytes;
+    unsigned nBlocks;
+};
+
+template <bool LZ, int P, int Q, int T, int OFF, int NP, int PD>
+__global__ __launch_bounds__(512) void ryx_kernel(RyxArgs a)
+{
+    constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
+    constexpr int NW = (SPAN + P - 1) / P * P;    // register window rows (whole groups of P)
+    constexpr int U = NW / P;                     // groups per unrolled trip (window slots repeat)
+    constexpr int OOB = 0x7ff00000;
+    constexpr int PADB = 2 * kRyxPadK;            // work-row byte padding left of column 0
+    static_assert(U % PD == 0, "prefetch slots repeat within a trip");
+    const RyxDev &d = a.d;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int t = static_cast<int>(threadIdx.x);
+    const unsigned blk = xcd_spread(blockIdx.x, gridDim.x);
+    if (blk >= a.nBlocks)
+        return;  // whole workgroup
+    const int band = static_cast<int>(blk % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(blk / static_cast<unsigned>(a.bands));
+    const int yb = a.groupBegin + band * a.rowsPerBand;  // a multiple of Q: first row of group mLo
+    const int y0 = max(yb, a.rowBegin), y1 = min(yb + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;  // whole workgroup
+    const int mLo = yb / Q;
+    const int nG = (y1 - yb + Q - 1) / Q;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+    const int voff = 4 * t < d.srcW ? 4 * t : OOB;
+
+    // work rows: two buffers of (pad + srcW + pad) u16, zero padding written once
+    const int pitch = PADB + 2 * d.srcW + PADB;
+    for (int i = t; i < 2 * (PADB / 4); i += 512) {
+        const int buf = i / (PADB / 4), k = i % (PADB / 4);
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * d.srcW + 4 * k) = 0u;
+    }
+    // this thread's two output columns: table entries for the whole band
+    const int x0 = 2 * t;
+    uint32_t cf[2][NP];
+    int aoff[2];
+    uint32_t mm[2];
+    int sh[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int x = min(x0 + k, d.dstW - 1);
+        const int4 c = d.cols[x];
+        aoff[k] = c.x;
+        mm[k] = static_cast<uint32_t>(c.y);
+        sh[k] = c.z;
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+            cf[k][q] = d.colCoef[x * NP + q];
+    }
+    const int stoff = x0 < d.dstW ? x0 : OOB;  // dstW is even (launch_ryx)
+
+    // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1
+    const int rBase = P * mLo + OFF;
+    const int rLast = P * (mLo + nG - 1) + OFF + SPAN - 1;
+    const int srcLast = a.io.srcRowEnd - 1;
+    auto load_row = [&](int q) -> uint32_t {
+        const int r = rBase + q;
+        const int rc = min(max(r, srcRow0), srcLast);
+        const bool in = r >= 0 && r < d.srcH && r <= rLast;
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
+        W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
+        W[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
+    };
+
+    uint32_t R[NW][2];
+#pragma unroll
+    for (int q = 0; q < SPAN - P; ++q)
+        widen(load_row(q), R[q]);
+    uint32_t pre[PD][P];
+#pragma unroll
+    for (int v = 0; v < PD; ++v)
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            pre[v][i] = load_row(SPAN - P + P * v + i);
+
+    int row = 0;  // output rows emitted by this workgroup: work buffer parity
+    for (int base = 0; base < nG; base += U) {
+        static_for<U>([&](auto vc) {
+            constexpr int v = decltype(vc)::value;
+            const int g = base + v;
+            if (g >= nG)
+                return;  // whole workgroup
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+                widen(pre[v % PD][i], R[(P * v + SPAN - P + i) % NW]);
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+                pre[v % PD][i] = load_row(SPAN - P + P * (g + PD) + i);
+            static_for<Q>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                constexpr int S0 = (P * j) / Q;  // window row of tap 0
+                const int y = Q * (mLo + g) + j;
+                // vertical: phase j's taps (scalar loads of the splats)
+                uint32_t W[2] = {0u, 0u};
+#pragma unroll
+                for (int k = 0; k < T; ++k) {
+                    const uint32_t c = static_cast<uint32_t>(sld(d.rowCoef, j * T + k));
+                    W[0] = pk_mad(R[(P * v + S0 + k) % NW][0], c, W[0]);
+                    W[1] = pk_mad(R[(P * v + S0 + k) % NW][1], c, W[1]);
+                }
+                if (LZ && (y < d.m0 || y >= d.m1)) {
+                    // masked border row (uniform, rare): rows outside the image read as zero
+                    const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
+                    W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
+                    W[1] = ydiv2(W[1], d.yM[side][i], d.yS[side][i]);
+                }
+                uint8_t *wr = lds + (row & 1) * pitch;
+                if (4 * t < d.srcW)
+                    *reinterpret_cast<uint2 *>(wr + PADB + 8 * t) = make_uint2(W[0], W[1]);
+                __syncthreads();
+                // horizontal: the thread's two columns
+                int o[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const uint32_t *w = reinterpret_cast<const uint32_t *>(wr + aoff[k]);
+                    if constexpr (LZ) {
+                        int acc = 1 << 19;
+#pragma unroll
+                        for (int q = 0; q < NP; ++q)
+                            acc = sdot2(w[q], cf[k][q], acc);
+                        o[k] = static_cast<int>(min(__umulhi(static_cast<uint32_t>(max(acc, 0)), mm[k]) >> sh[k], 255u));
+                    } else {
+                        uint32_t acc = 1u << 22;
+#pragma unroll
+                        for (int q = 0; q < NP; ++q)
+                            acc = udot2(w[q], cf[k][q], acc);
+                        const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
+                        o[k] = u > 255 ? 255 : u;
+                    }
+                }
+                const bool ok = y >= y0 && y < y1;
+                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(opaque(static_cast<uint32_t>(o[0])) |
+                                                                            (opaque(static_cast<uint32_t>(o[1])) << 8)),
+                                                      dstR, stoff + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+                ++row;
+            });
+        });
     }
 }
 
@@ -3348,6 +3834,101 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
 }
 
+hipError_t launch_d31(const D31Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.dstW % 4 || d.dstW < 16 || d.srcW != 3 * d.dstW)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    // producing lanes per wave (4 outputs each): the fewest waves per row, then the fewest lanes
+    // that tile the width
+    const int lanes = d.dstW / 4;
+    int wpr = (lanes + 61) / 62;
+    int np = d.np > 0 ? min(d.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
+    wpr = (lanes + np - 1) / np;
+    const void *kern = nullptr;
+    if (d.variant == 0)
+        kern = d.pd == 5 ? reinterpret_cast<const void *>(lanczos_d31_kernel<5, 0>)
+                         : reinterpret_cast<const void *>(lanczos_d31_kernel<1, 0>);
+    else if (d.variant == 1)
+        kern = d.pd == 2   ? reinterpret_cast<const void *>(lanczos_d31_kernel<2, 1>)
+               : d.pd == 4 ? reinterpret_cast<const void *>(lanczos_d31_kernel<4, 1>)
+                           : reinterpret_cast<const void *>(lanczos_d31_kernel<1, 1>);
+    else
+        return hipErrorInvalidValue;
+    const int rows = rowEnd - rowBegin;
+    const int trip = d.variant == 0 ? 5 : 4;  // output rows per unrolled trip (U)
+    // bands: ~2.5 rounds of resident waves, whole trips per band, >= 16 rows
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
+        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
+    }
+    bands = std::max(1, std::min(bands, (rows + trip - 1) / trip));
+    int rpb = (rows + bands - 1) / bands;
+    rpb = (rpb + trip - 1) / trip * trip;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
+    if (nWaves >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    D31Args a{d, io, rowBegin, rowEnd, rpb, bands, wpr, np, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nWaves)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>((nWaves + 3) / 4)), dim3(256), args, 0, s);
+}
+
+hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.srcW % 4 || d.srcW > 2048 || d.dstW > 1024 || d.dstW % 2)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    // instantiations (plan.cpp build_ryx kShapes): method, P, Q, taps
+    const void *kern = nullptr;
+    int trip = 0;
+    if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 14 && (d.NP == 8 || d.NP == 10)) {
+        kern = d.NP == 8 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 14, -6, 8, 1>)
+                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 14, -6, 10, 1>);
+        trip = 4 * 3;
+    } else if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 10 && (d.NP == 6 || d.NP == 7)) {
+        kern = d.NP == 6 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 10, -4, 6, 1>)
+                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 10, -4, 7, 1>);
+        trip = 4 * 2;
+    } else if (!d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 4 && d.NP == 3) {
+        kern = reinterpret_cast<const void *>(ryx_kernel<false, 9, 4, 4, 0, 3, 1>);
+        trip = 4 * 2;
+    } else {
+        return hipErrorInvalidValue;
+    }
+    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * d.srcW);
+    const int groupBegin = rowBegin - rowBegin % d.Q;
+    const int rows = rowEnd - groupBegin;
+    // bands: ~2.5 rounds of resident workgroups, whole trips per band
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, 512, ldsBytes) / 8);
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + io.frames - 1) / io.frames, std::max(1, rows / trip)));
+    }
+    bands = std::max(1, std::min(bands, (rows + d.Q - 1) / d.Q));
+    int rpb = (rows + bands - 1) / bands;
+    rpb = (rpb + d.Q - 1) / d.Q * d.Q;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames);
+    if (nBlocks >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    RyxArgs a{d, io, rowBegin, rowEnd, groupBegin, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nBlocks)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(512), args, static_cast<size_t>(ldsBytes), s);
+}
+
 hipError_t launch_u23(const U23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
@@ -3515,15 +4096,20 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int cpw = (chunks + wpr - 1) / wpr;
     const int rowPitch = l.ringPack ? rowNeed : 16 + 1024 * chunks;
     const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
+    // persistent XCD sweep (kernels.hip lanczos_symb_kernel): one-wave-row-per-band layouts only
+    const bool sweep = shared && l.sweep != 0;
     if (shared) {
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         const int K = pd <= 2 ? 3 : pd == 3 ? 4 : 5;
         ldsBytes = K * 2 * rowPitch + 2 * IQO_SYMB_EDGE_BATCH * 16 + (cpw * wpr > chunks ? 1024 : 0);
         block = 64 * wpr;
+#define IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, M_)                                                         \
+    (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 1, ONE_, M_>)                \
+              : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 2, ONE_, M_>))
 #define IQO_SYMB_K(NY_, NX_, OX_, K_, ONE_)                                                             \
-    (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 1, ONE_>)             \
-              : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 2, ONE_>))
+    (sweep ? IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, 2)                                                     \
+           : l.nt ? IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, 1) : IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, 0))
 #define IQO_SYMB(NY_, NX_, OX_, ONE_)                                                                   \
     (K == 3 ? IQO_SYMB_K(NY_, NX_, OX_, 3, ONE_) : K == 4 ? IQO_SYMB_K(NY_, NX_, OX_, 4, ONE_)          \
             : IQO_SYMB_K(NY_, NX_, OX_, 5, ONE_))
@@ -3535,6 +4121,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB
 #undef IQO_SYMB_K
+#undef IQO_SYMB_M
     } else if (l.sym) {
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         if (l.NY == 10 && one)
@@ -3558,7 +4145,30 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
                : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 2>)
                          : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 3>);
     }
-    if (bands <= 0) {
+    int sweepGrid = 0;
+    if (sweep) {
+        // resident workgroups (optionally fewer per CU), one band of ~34 rows per workgroup and at
+        // least one item per workgroup: 32 bands per frame on large batches
+        int cus = 256;
+        {
+            int dev = 0;
+            hipDeviceProp_t prop;
+            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                cus = prop.multiProcessorCount;
+        }
+        const int residentWg = std::max(1, resident_waves(kern, block, ldsBytes) / wpr);
+        const int wgs = l.sweepWg > 0 ? std::min(residentWg, l.sweepWg * cus) : residentWg;
+        if (bands <= 0)
+            bands = std::min(std::max(32, (wgs + io.frames - 1) / io.frames), std::max(1, rows / 8));
+        bands = max(1, min(bands, rows));
+        const int rpb0 = (rows + bands - 1) / bands;
+        bands = (rows + rpb0 - 1) / rpb0;
+        const int64_t items = static_cast<int64_t>(bands) * io.frames;
+        int64_t g = std::min<int64_t>(wgs, items);
+        if (g >= 8)
+            g -= g % 8;
+        sweepGrid = static_cast<int>(g);
+    } else if (bands <= 0) {
         const int resident = resident_waves(kern, block, ldsBytes);
         if (shared && l.rounds >= 0) {
             // block-shared ring: about `rounds` rounds of resident workgroups (default 6), bands of
@@ -3577,7 +4187,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
     a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd,
-                    l.ringPack ? lastLanes : 64};
+                    l.ringPack ? lastLanes : 64, sweep ? 1 : 0, io.frames, sweep ? 1 : 0};
     // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -3588,12 +4198,13 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
-    P->grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
-                     : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    P->grid = sweep    ? dim3(static_cast<unsigned>(sweepGrid))
+              : shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
+                       : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
     P->block = block;
     P->lds = ldsBytes;
     P->kern = kern;
-    P->kind = shared ? 1 : (l.sym ? 2 : 0);
+    P->kind = shared ? (sweep ? 3 : 1) : (l.sym ? 2 : 0);
     P->pd = pd;
     return hipSuccess;
 }
@@ -3611,16 +4222,29 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
     return hipLaunchKernel(P.kern, P.grid, dim3(static_cast<unsigned>(P.block)), args, static_cast<size_t>(P.lds), s);
 }
 
+// instantiations of area_int_kernel: <4,4> <2,2> <2,*> <4,*> <8,*> <3,3> <3,*> <6,*>
+constexpr int kAreaKinds = 8;
+int area_kind(const AreaDev &g)
+{
+    if (g.KX == 3)
+        return g.KY == 3 ? 5 : 6;
+    if (g.KX == 6)
+        return 7;
+    return g.KX == 4 && g.KY == 4 ? 0 : g.KX == 2 && g.KY == 2 ? 1 : g.KX == 2 ? 2 : g.KX == 4 ? 3 : 4;
+}
+
 hipError_t prep_area(const AreaDev &g, const Io &io, int rowBegin, int rowEnd, Prep<AreaArgs> *P)
 {
-    P->a = AreaArgs{g, io, rowBegin, rowEnd, g.srcW / 16};
+    const int cols = 16 % g.KX == 0 ? 16 : 12;  // source columns per thread (area_int_kernel_body)
+    P->a = AreaArgs{g, io, rowBegin, rowEnd, g.srcW / cols};
     const int64_t total = static_cast<int64_t>(rowEnd - rowBegin) * P->a.groups;
     P->grid = dim3(static_cast<unsigned>((total + 255) / 256), static_cast<unsigned>(io.frames));
-    P->kind = g.KX == 4 && g.KY == 4 ? 0 : g.KX == 2 && g.KY == 2 ? 1 : g.KX == 2 ? 2 : g.KX == 4 ? 3 : 4;
-    static const void *const kerns[5] = {
+    P->kind = area_kind(g);
+    static const void *const kerns[kAreaKinds] = {
         reinterpret_cast<const void *>(area_int_kernel<4, 4>), reinterpret_cast<const void *>(area_int_kernel<2, 2>),
         reinterpret_cast<const void *>(area_int_kernel<2, 0>), reinterpret_cast<const void *>(area_int_kernel<4, 0>),
-        reinterpret_cast<const void *>(area_int_kernel<8, 0>)};
+        reinterpret_cast<const void *>(area_int_kernel<8, 0>), reinterpret_cast<const void *>(area_int_kernel<3, 3>),
+        reinterpret_cast<const void *>(area_int_kernel<3, 0>), reinterpret_cast<const void *>(area_int_kernel<6, 0>)};
     P->kern = kerns[P->kind];
     return hipSuccess;
 }
@@ -3716,7 +4340,9 @@ hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const Lanc
         return hipErrorInvalidValue;
     Prep<LanczosArgs> py, pu, pv;
     hipError_t e;
-    if ((e = prep_lanczos(ly, ioY, 0, ly.dstH, 0, &py)) != hipSuccess ||
+    LanczosDev lyGrid = ly;
+    lyGrid.sweep = 0;  // the fused launch needs the (band, frame) grid of every plane
+    if ((e = prep_lanczos(lyGrid, ioY, 0, ly.dstH, 0, &py)) != hipSuccess ||
         (e = prep_lanczos(lc, ioU, 0, lc.dstH, 0, &pu)) != hipSuccess ||
         (e = prep_lanczos(lc, ioV, 0, lc.dstH, 0, &pv)) != hipSuccess)
         return e;
@@ -3737,7 +4363,7 @@ hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const Lanc
         return hipErrorNotSupported;
     if (!shared && py.kind == 1) {
         // re-prepare Y as the per-wave symmetric streamer (256-thread blocks of 4 waves)
-        LanczosDev l2 = ly;
+        LanczosDev l2 = lyGrid;
         l2.sym = 2;
         if ((e = prep_lanczos(l2, ioY, 0, ly.dstH, 0, &py)) != hipSuccess)
             return e;
@@ -3757,14 +4383,17 @@ hipError_t launch_yuv420_area(const AreaDev &gy, const Io &ioY, const AreaDev &g
     (void)prep_area(gy, ioY, 0, gy.dstH, &py);
     (void)prep_area(gc, ioU, 0, gc.dstH, &pu);
     (void)prep_area(gc, ioV, 0, gc.dstH, &pv);
-    if (py.kind != pu.kind || (py.kind >= 2 && gy.KY != gc.KY))
+    if (py.kind != pu.kind || (py.kind >= 2 && py.kind != 5 && gy.KY != gc.KY))
         return hipErrorNotSupported;
-    static const void *const kerns[5] = {
+    static const void *const kerns[kAreaKinds] = {
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<4, 4>, AreaArgs>),
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<2, 2>, AreaArgs>),
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<2, 0>, AreaArgs>),
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<4, 0>, AreaArgs>),
-        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<8, 0>, AreaArgs>)};
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<8, 0>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<3, 3>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<3, 0>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<6, 0>, AreaArgs>)};
     return launch_fused3(kerns[py.kind], py, pu, pv, 256, 0, s);
 }
 

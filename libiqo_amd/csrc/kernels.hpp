@@ -97,6 +97,37 @@ struct D32Dev {
 };
 hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
+// Exact 3:1 Lanczos-2/3 downscale (plan.hpp D31Tables): every row and column.
+struct D31Dev {
+    int srcW, srcH, dstW, dstH;
+    int np;                      // producing lanes per wave (0 = auto)
+    int pd;                      // output rows loaded ahead (Lanczos-3: 1, 5; Lanczos-2: 1, 2, 4; 0 = 1)
+    int variant;                 // tap structure: 0 Lanczos-3 (18 taps), 1 Lanczos-2 (12 taps)
+    uint32_t cc, cp[5];          // (c, c) u16 splats: the centre tap, the symmetric pairs' taps
+    uint32_t cxe[9], cxo[9];     // (c_2q, c_2q+1) / (c_2q+1, c_2q+2) int16 pairs: even / odd window starts
+    uint32_t xM[2][4];           // edge-lane exact divisions (left / right 4 columns)
+    int xT[2][4];
+    int m0, m1;                  // main rows; the others are masked border rows divided by
+    uint32_t yM[2][8];           //   magic_y (top: row y, bottom: row y - m1)
+    int yS[2][8];
+};
+hipError_t launch_d31(const D31Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
+// Exact vertical ratio, tabled columns (plan.hpp RyxTables): every row and column.
+constexpr int kRyxPadK = 16;     // work-row padding (u16 entries) left of column 0: plan.hpp kRyxPad
+struct RyxDev {
+    bool lanczos;
+    int srcW, srcH, dstW, dstH;
+    int P, Q, taps, NP;
+    int m0, m1;                  // Lanczos main rows; the others are masked border rows (magic_y)
+    uint32_t yM[2][8];
+    int yS[2][8];
+    const uint32_t *rowCoef;     // Q x taps (c, c) splats
+    const int4 *cols;            // per column {work byte offset of the even start, magic, shift, 0}
+    const uint32_t *colCoef;     // dstW x NP pairs
+};
+hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
 // Exact 2:3 Lanczos-3 upscale (plan.hpp U23Tables).
 struct U23Dev {
     int srcW, srcH, dstW, dstH;
@@ -156,6 +187,10 @@ struct LanczosDev {
     int ringPack;                // block-shared streamer: ring rows packed to the bytes they need
     int rounds;                  // block-shared streamer: target rounds of resident workgroups for the
                                  // auto band count (0 = default 6, -1 = one-round makespan model)
+    int sweep;                   // block-shared streamer: 1 = persistent XCD sweep with nontemporal
+                                 // streams (default), 0 = one workgroup per (band, frame)
+    int sweepWg;                 // sweep: workgroups per CU (0 = as many as are resident)
+    int nt;                      // grid layout: nontemporal source loads and output stores
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,

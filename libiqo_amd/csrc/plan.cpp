@@ -4,6 +4,7 @@
 #include "plan.hpp"
 
 #include <algorithm>
+#include <numeric>
 #include <cmath>
 #include <cstdlib>
 
@@ -553,9 +554,10 @@ void pick_fast_area(Plan *p)
     if (p->srcW % p->dstW || p->srcH % p->dstH)
         return;
     int KX = p->srcW / p->dstW, KY = p->srcH / p->dstH;
-    if (!(KX == 2 || KX == 4 || KX == 8) || KY < 2 || KY > 16 || x.taps != KX || y.taps != KY)
+    if (!(KX == 2 || KX == 3 || KX == 4 || KX == 6 || KX == 8) || KY < 2 || KY > 16 || x.taps != KX || y.taps != KY)
         return;
-    if (p->srcW % 32)
+    // kernels.hip area_int_kernel: a thread takes 16 source columns (12 when KX is 3 or 6)
+    if (p->srcW % ((16 % KX == 0) ? 32 : 12))
         return;
     p->far.KX = KX;
     p->far.KY = KY;
@@ -1303,6 +1305,218 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
         for (int q = 0; q < S.NPX; ++q)
             d->cx[ph][q] = (static_cast<uint32_t>(tap(ph, 2 * q)) & 0xffffu) |
                            (static_cast<uint32_t>(tap(ph, 2 * q + 1)) << 16);
+    d->variant = vi;
+    d->m0 = m0;
+    d->m1 = m1;
+    d->ok = true;
+}
+
+void build_ryx(const Plan &p, RyxTables *t)
+{
+    *t = RyxTables();
+    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 2048 || p.dstW > 1024 || p.srcW % 4 ||
+        p.srcW < 16 || p.dstH < 4)
+        return;
+    // downscales only (the kernel's register window holds the rows of one group of Q outputs)
+    const int64_t g = std::gcd(static_cast<int64_t>(p.srcH), static_cast<int64_t>(p.dstH));
+    const int P = static_cast<int>(p.srcH / g), Q = static_cast<int>(p.dstH / g);
+    const int T = p.y.taps;
+    const int off = p.method == kLanczos ? 1 - T / 2 : 0;
+    // instantiated (P, Q, taps, method) shapes: kernels.hip launch_ryx
+    struct Shape {
+        int method, P, Q, T, NP;
+    };
+    static const Shape kShapes[] = {{kLanczos, 9, 4, 14, 8}, {kLanczos, 9, 4, 14, 10}, {kLanczos, 9, 4, 10, 6},
+                                    {kLanczos, 9, 4, 10, 7}, {kArea, 9, 4, 4, 3}};
+    int NP = 0;  // the fewest pairs that hold every column window
+    for (const Shape &S : kShapes)
+        if (S.method == p.method && S.P == P && S.Q == Q && S.T == T && p.x.taps + 1 <= 2 * S.NP && !NP)
+            NP = S.NP;
+    // the column windows (an odd start takes one more entry) must fit the instantiation's NP pairs
+    if (!NP || p.y.phases != Q || p.x.taps + 1 > 2 * NP)
+        return;
+    // rows: every window starts at P m + floor(P j / Q) + off and takes phase j
+    for (int y = 0; y < p.dstH; ++y) {
+        const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
+        const int m = y / Q, j = y % Q;
+        if (ci.kind == kIdentity || ci.srcO != P * m + (P * j) / Q + off || ci.tabOff != j * T)
+            return;
+    }
+    t->rowCoef.resize(static_cast<size_t>(Q * T));
+    for (int k = 0; k < Q * T; ++k) {
+        const uint32_t c = static_cast<uint32_t>(p.y.table[static_cast<size_t>(k)]) & 0xffffu;
+        t->rowCoef[static_cast<size_t>(k)] = c * 0x10001u;
+    }
+    int m0 = 0, m1 = p.dstH;
+    if (p.method == kLanczos) {
+        m0 = -1;
+        m1 = -1;
+        for (int y = 0; y < p.dstH; ++y) {
+            const Window win = axis_window(p, p.y, y, false);
+            if (!win.border) {
+                if (win.start < 0 || win.start + T > p.srcH)
+                    return;
+                if (m0 < 0)
+                    m0 = y;
+                else if (m1 >= 0)
+                    return;
+            } else if (m0 >= 0 && m1 < 0) {
+                m1 = y;
+            }
+        }
+        if (m0 < 0)
+            return;
+        if (m1 < 0)
+            m1 = p.dstH;
+        if (m0 > 8 || p.dstH - m1 > 8)
+            return;
+        for (int y = 0; y < p.dstH; ++y) {
+            if (y >= m0 && y < m1)
+                continue;
+            const Window win = axis_window(p, p.y, y, false);
+            const int side = y < m0 ? 0 : 1, i = side ? y - m1 : y;
+            if (!win.border || !magic_y(win.div, &t->yM[side][i], &t->yS[side][i]))
+                return;
+        }
+    }
+    // columns: the reference's window, made to start on an even column (a leading zero coefficient),
+    // NP pairs; masked Lanczos border taps outside the image meet the zero padding of the work row
+    t->cols.assign(static_cast<size_t>(p.dstW) * 4, 0);
+    t->colCoef.assign(static_cast<size_t>(p.dstW) * NP, 0u);
+    for (int x = 0; x < p.dstW; ++x) {
+        const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
+        if (ci.kind == kIdentity)
+            return;
+        const int start = ci.srcO;
+        const int a = start & ~1;  // even start (floor)
+        if (a < -kRyxPad || a + 2 * NP > p.srcW + kRyxPad)
+            return;
+        std::vector<int32_t> c(static_cast<size_t>(2 * NP), 0);
+        for (int k = 0; k < p.x.taps; ++k)
+            c[static_cast<size_t>(start - a + k)] = p.x.table[static_cast<size_t>(ci.tabOff + k)];
+        for (int q = 0; q < NP; ++q)
+            t->colCoef[static_cast<size_t>(x) * NP + q] = (static_cast<uint32_t>(c[static_cast<size_t>(2 * q)]) & 0xffffu) |
+                                                       (static_cast<uint32_t>(c[static_cast<size_t>(2 * q + 1)]) << 16);
+        uint32_t m = 0;
+        int32_t sh = 0;
+        if (p.method == kLanczos) {
+            const Window win = axis_window(p, p.x, x, true);
+            if (!magic_x(win.border ? win.div : (1 << 20), &m, &sh))
+                return;
+        }
+        int32_t *cx = &t->cols[static_cast<size_t>(x) * 4];
+        cx[0] = 2 * (a + kRyxPad);  // byte offset in the work row
+        cx[1] = static_cast<int32_t>(m);
+        cx[2] = sh;
+    }
+    t->P = P;
+    t->Q = Q;
+    t->taps = T;
+    t->off = off;
+    t->NP = NP;
+    t->m0 = m0;
+    t->m1 = m1;
+    t->ok = true;
+}
+
+void build_d31(const Plan &p, D31Tables *d)
+{
+    *d = D31Tables();
+    if (p.method != kLanczos || p.x.identity || p.y.identity || p.srcW != 3 * p.dstW || p.srcH != 3 * p.dstH ||
+        p.dstW % 4 || p.dstW < 16 || p.dstH < 8)
+        return;
+    // the instantiated tap structures (kernels.hip D31Shape): taps T, window start B relative to 3y,
+    // the symmetric pair distances about the centre tap T/2 (non-zero taps only), the zero taps
+    struct Shape {
+        int T, B, npy;
+        int dist[5];
+    };
+    static const Shape kShapes[2] = {{18, -8, 5, {1, 2, 4, 5, 7}}, {12, -5, 4, {1, 2, 4, 5, 0}}};
+    const int T = static_cast<int>(p.x.taps);
+    if (static_cast<int>(p.y.taps) != T || p.x.phases != 1 || p.y.phases != 1)
+        return;
+    int vi = -1;
+    for (int k = 0; k < 2; ++k)
+        if (kShapes[k].T == T)
+            vi = k;
+    if (vi < 0)
+        return;
+    const Shape &S = kShapes[vi];
+    const int C = T / 2;
+    // every window (main or masked border) starts at 3i + B and takes the one phase
+    for (const AxisPlan *ax : {&p.x, &p.y}) {
+        const bool isX = ax == &p.x;
+        for (int i = 0; i < ax->dstLen; ++i) {
+            const CoordInfo &ci = ax->coord[static_cast<size_t>(i)];
+            if (ci.kind == kIdentity || ci.tabOff != 0 || axis_window(p, *ax, i, isX).start != 3 * i + S.B)
+                return;
+        }
+    }
+    // the Y table: tap 0 zero, taps symmetric about C, non-zero only at C and C +- dist
+    const std::vector<int32_t> &ty = p.y.table, &tx = p.x.table;
+    if (ty[0] != 0 || tx[0] != 0)
+        return;
+    for (int k = 1; k < T; ++k) {
+        if (ty[static_cast<size_t>(k)] != ty[static_cast<size_t>(2 * C - k)])
+            return;
+        const int dist = k > C ? k - C : C - k;
+        bool used = dist == 0;
+        for (int q = 0; q < S.npy; ++q)
+            used = used || S.dist[q] == dist;
+        if (!used && ty[static_cast<size_t>(k)] != 0)
+            return;
+    }
+    // columns: border columns only among the 4 outermost on each side
+    for (int x = 0; x < p.dstW; ++x) {
+        const Window win = axis_window(p, p.x, x, true);
+        const int side = x < 4 ? 0 : x >= p.dstW - 4 ? 1 : -1;
+        if (win.border && side < 0)
+            return;
+        if (side >= 0) {
+            const int j = side ? x - (p.dstW - 4) : x;
+            if (!magic_x(win.border ? win.div : (1 << 20), &d->xM[side][j], &d->xT[side][j]))
+                return;
+        }
+    }
+    // rows: one contiguous run of main rows with at most 8 masked border rows above and below
+    int m0 = -1, m1 = -1;
+    for (int y = 0; y < p.dstH; ++y) {
+        const Window win = axis_window(p, p.y, y, false);
+        if (!win.border) {
+            if (win.start < 0 || win.start + T > p.srcH)
+                return;
+            if (m0 < 0)
+                m0 = y;
+            else if (m1 >= 0)
+                return;
+        } else if (m0 >= 0 && m1 < 0) {
+            m1 = y;
+        }
+    }
+    if (m0 < 0)
+        return;
+    if (m1 < 0)
+        m1 = p.dstH;
+    if (m0 > 8 || p.dstH - m1 > 8)
+        return;
+    for (int y = 0; y < p.dstH; ++y) {
+        if (y >= m0 && y < m1)
+            continue;
+        const Window win = axis_window(p, p.y, y, false);
+        const int side = y < m0 ? 0 : 1, i = side ? y - m1 : y;
+        if (!win.border || !magic_y(win.div, &d->yM[side][i], &d->yS[side][i]))
+            return;
+    }
+    auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
+    d->cc = splat(ty[static_cast<size_t>(C)]);
+    for (int q = 0; q < S.npy; ++q)
+        d->cp[q] = splat(ty[static_cast<size_t>(C + S.dist[q])]);
+    auto tap = [&](int k) { return k < T ? tx[static_cast<size_t>(k)] : 0; };
+    auto pr = [](int32_t lo, int32_t hi) { return (static_cast<uint32_t>(lo) & 0xffffu) | (static_cast<uint32_t>(hi) << 16); };
+    for (int q = 0; q < 9; ++q) {
+        d->cxe[q] = pr(tap(2 * q), tap(2 * q + 1));
+        d->cxo[q] = pr(tap(2 * q + 1), tap(2 * q + 2));
+    }
     d->variant = vi;
     d->m0 = m0;
     d->m1 = m1;

@@ -226,6 +226,45 @@ struct D32Tables {
 };
 void build_d32(const Plan &p, const WalkTables &w, D32Tables *d);
 
+// Exact 3:1 Lanczos-2/3 downscale (kernels.hip lanczos_d31_kernel), e.g. 3840x2160 -> 1280x720.  In
+// the reference's tables for this ratio output y (x) takes the single phase's T taps (18 / 12) from
+// source row 3y + B (B = -8 / -5); tap 0 is zero and taps 1 .. T-1 are symmetric about the centre
+// tap T/2, so a row is the centre row times its coefficient plus pair sums times theirs.  Border
+// rows / columns (<= 8 rows, <= 4 columns per side) are masked in the kernel.
+struct D31Tables {
+    bool ok = false;
+    int variant = 0;                // 0 Lanczos-3 (18 taps), 1 Lanczos-2 (12 taps)
+    int m0 = 0, m1 = 0;             // main rows; the others are masked border rows
+    uint32_t cc = 0, cp[5] = {};    // (c, c) u16 splats: centre tap, symmetric pair taps (kernel order)
+    uint32_t cxe[9] = {}, cxo[9] = {};  // (c_2q, c_2q+1) / (c_2q+1, c_2q+2) int16 pairs
+    uint32_t xM[2][4] = {};         // edge lanes (left: columns 0..3, right: dstW - 4 ..)
+    int32_t xT[2][4] = {};
+    uint32_t yM[2][8] = {};         // border row y (top: y, bottom: y - m1)
+    int32_t yS[2][8] = {};
+};
+void build_d31(const Plan &p, D31Tables *t);
+
+// Exact vertical ratio P:Q, any horizontal ratio (kernels.hip ryx_kernel), e.g. 1920x1080 ->
+// 854x480 (Y 9:4, X 960:427).  Rows: output y = Q m + j reads the taps of phase j from source row
+// P m + floor(P j / Q) + OFF (OFF = 1 - taps/2 for Lanczos, 0 for Area); the vertical pass keeps a
+// register window of source rows.  Columns: every output column's window (even start, a leading
+// zero coefficient when the reference's start is odd) and coefficient pairs come from a table, with
+// an exact division constant per column (Lanczos border columns; the identity 2^20 elsewhere).
+struct RyxTables {
+    bool ok = false;
+    int P = 0, Q = 0, taps = 0, off = 0;   // the instantiation this plan needs (kernels.hip kRyxShapes)
+    int NP = 0;                            // coefficient pairs per column
+    int m0 = 0, m1 = 0;                    // Lanczos main rows; the others are masked border rows
+    uint32_t yM[2][8] = {};                // border row y (top: y, bottom: y - m1): magic_y
+    int32_t yS[2][8] = {};
+    std::vector<uint32_t> rowCoef;         // Q x taps (c, c) u16 splats: phase j's taps
+    std::vector<int32_t> cols;             // dstW x 4: {work byte offset of the even start, magic, shift, 0}
+    std::vector<uint32_t> colCoef;         // dstW x NP coefficient pairs from the even start
+};
+// Work-row padding (u16 entries) left of source column 0 in the kernel's LDS work row.
+constexpr int kRyxPad = 16;
+void build_ryx(const Plan &p, RyxTables *t);
+
 // Exact 2:3 Lanczos-3 upscale (kernels.hip lanczos_u23_kernel), e.g. 1280x720 -> 1920x1080.  In the
 // reference's tables for this ratio output y (x) = 3m + j takes phase j: j = 0 a single tap on
 // source row 2m, j = 1 six taps from 2m - 2, j = 2 six taps from 2m - 1 (at the masked borders

@@ -4,13 +4,13 @@
 # objects shared).  -DIQO_VARIANT_DEBUG enables the wrong-output timing flags ("debug_flags").
 set -e
 cd "$(dirname "$0")/../libiqo_amd"
-make -s build/plan.o build/resizers.o
+make -s build/plan.o build/cpu_generic.o build/resizers.o
 mkdir -p variants
 F="-O3 -std=c++17 -fPIC -fno-strict-aliasing -I../include -Icsrc --offload-arch=gfx950 $2"
 /opt/rocm/bin/hipcc $F -c csrc/kernels.hip -o variants/$1_kernels.o &
 /opt/rocm/bin/hipcc $F -ffp-contract=off -c csrc/abi.hip -o variants/$1_abi.o
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/$1.so build/plan.o build/resizers.o \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o variants/$1.so build/plan.o build/cpu_generic.o build/resizers.o \
     variants/$1_kernels.o variants/$1_abi.o
 rm -f variants/$1_kernels.o variants/$1_abi.o
 echo "variants/$1.so"

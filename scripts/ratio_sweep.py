@@ -30,6 +30,13 @@ SHAPES = [
     ("area", 0, 1920, 1080, 854, 480),
     ("linear", 0, 1920, 1080, 3840, 2160),
     ("linear", 0, 1280, 720, 1920, 1080),
+    # round 3: exact 3:1 (lanczos_d31, area_int with 12-column threads)
+    ("lanczos", 2, 3840, 2160, 1280, 720),
+    ("area", 0, 3840, 2160, 1280, 720),
+    ("lanczos", 3, 1920, 1080, 640, 360),
+    # round 3: exact vertical ratio, tabled columns (ryx)
+    ("lanczos", 2, 1920, 1080, 854, 480),
+    ("lanczos", 3, 1920, 1080, 640, 480),
 ]
 
 

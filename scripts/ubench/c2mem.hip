@@ -60,9 +60,18 @@ __global__ __launch_bounds__(256) void c2mem(const uint8_t *src, uint8_t *dst, P
     unsigned acc = 0;
     const int G = p.persistent ? p.persistent : nItems;
     const int start = p.persistent ? (int)xcd_spread(blockIdx.x, G) : (int)blockIdx.x;
-    for (int it = start; it < nItems; it += G) {
+    // order 4 (persistent only): XCD x sweeps the frames x, x + 8, ... in order; its items are
+    // (frame, band) pairs frame-major, i -> (x + 8 (i / B), i % B), and its g4 workgroups take
+    // i = j, j + g4, ... (a compact window per XCD: g4 / B frames in flight)
+    const int g4 = G >> 3, j4 = (int)(blockIdx.x >> 3), x4 = (int)(blockIdx.x & 7);
+    int i4 = j4;
+    for (int it = start; p.order == 4 ? (x4 + 8 * (i4 / p.B)) < p.F : it < nItems; it += G) {
         int f, b;
-        if (p.order == 0) { f = it / p.B; b = it % p.B; }
+        if (p.order == 4) {
+            f = x4 + 8 * (i4 / p.B);
+            b = i4 % p.B;
+            i4 += g4;
+        } else if (p.order == 0) { f = it / p.B; b = it % p.B; }
         else if (p.order == 1 || p.order == 3) { const int l = p.persistent ? it : (int)xcd_spread(it, nItems); f = l / p.B; b = l % p.B; }
         else { f = it % p.F; b = it / p.F; }
         int y0, y1;
@@ -196,6 +205,42 @@ int main(int argc, char **argv)
             }
         return 0;
     }
+    if (!strcmp(only, "v3")) {
+        // nontemporal loads + stores (the best r2 policy) over grids, band counts, persistence, orders
+        for (int rep = 0; rep < 2; ++rep) {
+            if (!strcmp(argc > 2 ? argv[2] : "", "sweep")) goto sweep;
+            for (int G : {256, 512, 768, 1024})
+                for (int B : {24, 48, 72, 135}) {
+                    char tag[64];
+                    snprintf(tag, sizeof tag, "ntl nts persistent rep%d", rep);
+                    t(c2mem<4, true, 0, 1>, 4, true, mk(B, 1, G, 1, 0, 1, 1), G / 256, tag);
+                }
+            for (int perCU : {1, 2, 4})
+                for (int B : {48, 135}) {
+                    char tag[64];
+                    snprintf(tag, sizeof tag, "ntl nts one item per WG rep%d", rep);
+                    t(c2mem<4, true, 0, 1>, 4, true, mk(B, 1, 0, 1, 0, 1, 1), perCU, tag);
+                }
+        sweep:
+            for (int G : {256, 512, 1024})
+                for (int B : {8, 16, 24, 32, 48, 64}) {
+                    const int R = (DH + B - 1) / B;
+                    t(c2mem<4, true, 0, 1>, 4, true, P{F, B, R, 1, 1, 4, G, 0, 0}, G / 256, "ntl nts xcd-sweep");
+                    if (B == 32) {
+                        t(c2mem<4, true, 0, 0>, 4, true, P{F, B, R, 0, 0, 4, G, 0, 0}, G / 256, "xcd-sweep");
+                        t(c2mem<4, true, 0, 1>, 4, true, P{F, B, R, 0, 1, 4, G, 0, 0}, G / 256, "nts xcd-sweep");
+                        t(c2mem<4, true, 0, 0>, 4, true, P{F, B, R, 1, 0, 4, G, 0, 0}, G / 256, "ntl xcd-sweep");
+                        t(c2mem<4, true, 0, 1>, 4, true, P{F, B, R, 1, 1, 4, G, 1, 0}, G / 256, "ntl nts xcd-sweep alt");
+                    }
+                }
+            t(c2mem<4, true, 0, 1>, 4, true, mk(48, 1, 256, 0, 0, 1, 1), 1, "ntl nts persistent no-alt");
+            t(c2mem<2, true, 0, 1>, 2, true, mk(48, 1, 256, 1, 0, 1, 1), 1, "ntl nts persistent D2");
+            t(c2mem<3, true, 0, 1>, 3, true, mk(48, 1, 256, 1, 0, 1, 1), 1, "ntl nts persistent D3");
+            t(c2mem<6, true, 0, 1>, 6, true, mk(48, 1, 256, 1, 0, 1, 1), 1, "ntl nts persistent D6");
+            t(c2mem<4, true, 0, 1>, 4, true, mk(48, 1, 256, 1, 0, 0, 1), 1, "nts persistent");
+        }
+        return 0;
+    }
     // store forms and cache policies on the two best r1 schedules (persistent 256 B48; 4/CU B135)
     for (int sched = 0; sched < 2; ++sched) {
         const int B = sched ? 135 : 48, pers = sched ? 0 : 256, perCU = sched ? 4 : 1;
@@ -218,6 +263,12 @@ int main(int argc, char **argv)
         t(c2mem<4, true, 0>, 4, true, mk(B, 1, pers, 1, 1, 1, 0), perCU, "no stores ntl");
     }
     // persistent grid sizes and band counts with 16-B paired stores
+    // per-XCD frame sweeps with R-row items taken round-robin (compact window per XCD)
+    for (int G : {256, 512, 1024})
+        for (int R : {2, 4, 8, 16}) {
+            const int B = (DH + R - 1) / R;
+            t(c2mem<4, true, 1>, 4, true, P{F, B, R, 0, 0, 4, G, 0, 0}, G / 256, "st16pair xcd-sweep");
+        }
     for (int G : {256, 512})
         for (int B : {24, 36, 48, 72}) {
             const int perCU = G / 256;

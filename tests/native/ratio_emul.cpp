@@ -1,5 +1,5 @@
 // Test-only scalar emulation of the exact-ratio kernels of kernels.hip (lanczos_d32_kernel,
-// lanczos_up2_kernel, area_d32_kernel) over the product's own tables (libiqo_amd/csrc/plan.cpp
+// lanczos_up2_kernel, area_d32_kernel, lanczos_u23_kernel, linear_u23_kernel, lanczos_d31_kernel) over the product's own tables (libiqo_amd/csrc/plan.cpp
 // build_d32 / build_up2 / build_a32), so the coordinate checks, the zero rows / columns outside
 // the image, the magic-number border divisions and the edge-lane rewrite are checked against the
 // oracle on a machine without a GPU.  Emulates the kernels' arithmetic word for word: 16-bit
@@ -37,7 +37,7 @@ uint8_t edge_div(int s, uint32_t m, int t)
 
 extern "C" {
 
-// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23.  Returns 0 on success, 1 if the shape is
+// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23, 4 = linear_u23, 5 = lanczos_d31, 6 = ryx.  Returns 0 on success, 1 if the shape is
 // not eligible for that kernel, -1 on bad arguments.
 int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int dstW, int dstH, int pxScale,
                const uint8_t *src, uint8_t *dst)
@@ -187,6 +187,89 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
                 const int g = x / 3, q = x % 3, a = 2 * g + q - 1;
                 const uint32_t s = (1u << 22) + Wc(a) * (l.cx[q] & 0xffffu) + Wc(a + 1) * (l.cx[q] >> 16);
                 dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(sat_u8(static_cast<int>(s) >> 23));
+            }
+        }
+        return 0;
+    }
+    if (kind == 5) {
+        D31Tables d;
+        build_d31(p, &d);
+        if (!d.ok)
+            return 1;
+        // kernels.hip D31Shape: window rows 3y + YA .., centre CEN, pair distances; columns from 3x + XS
+        const int YA = d.variant ? -4 : -6, CEN = d.variant ? 5 : 7, NPY = d.variant ? 4 : 5;
+        const int DIST[5] = {1, 2, 4, 5, 7};
+        const int XS = d.variant ? -5 : -8, NPX = d.variant ? 6 : 9;
+        for (int y = 0; y < dstH; ++y) {
+            const int r0 = 3 * y + YA;
+            for (int c = 0; c < srcW; ++c) {
+                uint16_t acc = static_cast<uint16_t>(px(r0 + CEN, c) * static_cast<uint16_t>(d.cc));
+                for (int k = 0; k < NPY; ++k)
+                    acc = static_cast<uint16_t>(acc + (px(r0 + CEN - DIST[k], c) + px(r0 + CEN + DIST[k], c)) *
+                                                          static_cast<uint16_t>(d.cp[k]));
+                if (y < d.m0 || y >= d.m1) {
+                    const int side = y < d.m0 ? 0 : 1, bi = side ? y - d.m1 : y;
+                    acc = ydiv1(acc, d.yM[side][bi], d.yS[side][bi]);
+                }
+                work[static_cast<size_t>(c)] = acc;
+            }
+            auto W = [&](int c) -> int { return (c < 0 || c >= srcW) ? 0 : static_cast<int16_t>(work[static_cast<size_t>(c)]); };
+            for (int x = 0; x < dstW; ++x) {
+                const int st = 3 * x + XS;
+                const bool odd = (st & 1) != 0;
+                const int a = odd ? st + 1 : st;
+                int s = 1 << 19;
+                for (int q = 0; q < NPX; ++q) {
+                    const uint32_t cq = odd ? d.cxo[q] : d.cxe[q];
+                    s += W(a + 2 * q) * static_cast<int16_t>(cq & 0xffffu) + W(a + 2 * q + 1) * static_cast<int16_t>(cq >> 16);
+                }
+                const int side = x < 4 ? 0 : x >= dstW - 4 ? 1 : -1;
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(
+                    side < 0 ? sat_u8(s >> 20) : edge_div(s, d.xM[side][side ? x - (dstW - 4) : x], d.xT[side][side ? x - (dstW - 4) : x]));
+            }
+        }
+        return 0;
+    }
+    if (kind == 6) {
+        RyxTables r;
+        build_ryx(p, &r);
+        if (!r.ok)
+            return 1;
+        const bool lz = method == 0;
+        const int P = r.P, Q = r.Q, T = r.taps, NP = r.NP;
+        std::vector<uint16_t> wrow(static_cast<size_t>(srcW + 2 * kRyxPad), 0);
+        for (int y = 0; y < dstH; ++y) {
+            const int m = y / Q, j = y % Q, r0 = P * m + (P * j) / Q + r.off;
+            for (int c = 0; c < srcW; ++c) {
+                uint16_t acc = 0;
+                for (int k = 0; k < T; ++k)
+                    acc = static_cast<uint16_t>(acc + px(r0 + k, c) * static_cast<uint16_t>(r.rowCoef[static_cast<size_t>(j * T + k)]));
+                if (lz && (y < r.m0 || y >= r.m1)) {
+                    const int side = y < r.m0 ? 0 : 1, bi = side ? y - r.m1 : y;
+                    acc = ydiv1(acc, r.yM[side][bi], r.yS[side][bi]);
+                }
+                wrow[static_cast<size_t>(kRyxPad + c)] = acc;
+            }
+            for (int x = 0; x < dstW; ++x) {
+                const int32_t *cx = &r.cols[static_cast<size_t>(x) * 4];
+                const int a = cx[0] / 2;  // u16 index of the even start in the padded row
+                int64_t s = lz ? (1 << 19) : (1 << 22);
+                for (int q = 0; q < NP; ++q) {
+                    const uint32_t c = r.colCoef[static_cast<size_t>(x) * NP + q];
+                    const uint16_t w0 = wrow[static_cast<size_t>(a + 2 * q)], w1 = wrow[static_cast<size_t>(a + 2 * q + 1)];
+                    if (lz)
+                        s += static_cast<int16_t>(w0) * static_cast<int16_t>(c & 0xffffu) + static_cast<int16_t>(w1) * static_cast<int16_t>(c >> 16);
+                    else
+                        s += static_cast<int64_t>(w0) * (c & 0xffffu) + static_cast<int64_t>(w1) * (c >> 16);
+                }
+                uint8_t o;
+                if (lz) {
+                    o = edge_div(static_cast<int>(s), static_cast<uint32_t>(cx[1]), cx[2]);
+                } else {
+                    const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(static_cast<uint32_t>(s)) >> 23));
+                    o = static_cast<uint8_t>(u > 255 ? 255 : u);
+                }
+                dst[static_cast<size_t>(y) * dstW + x] = o;
             }
         }
         return 0;

@@ -51,7 +51,7 @@ def test_golden_vectors_gpu(golden, variant):
             continue
         r = libiqo_amd.make_resizer(c["method"], c["degree"], sw, sh, dw, dh, c["pxScale"])
         if variant == "tile":
-            for k in ("walk", "a32", "d32", "up2", "u23", "l23"):
+            for k in ("walk", "a32", "d32", "d31", "ryx", "up2", "u23", "l23"):
                 r.set_option(k, 0)
         elif variant != "default":
             r.set_option(variant, 1)
@@ -307,12 +307,21 @@ def test_stream_variants_agree_with_oracle(shape):
     exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 1, frames[f]) for f in range(2)]
     for variant, pd, lanes, bands in [(0, 1, 0, 0), (0, 2, 0, 7), (0, 3, 0, 0), (0, 2, 62, 3), (0, 3, 33, 0),
                                       (0, 3, 0, 1), (1, 3, 0, 0), (1, 1, 0, 5), (2, 3, 0, 0), (2, 1, 0, 5),
-                                      (2, 2, 40, 0), (3, 3, 0, 0), (3, 2, 0, 7), (3, 3, 41, 0), (3, 3, 0, 1)]:
+                                      (2, 2, 40, 0), (3, 3, 0, 0), (3, 2, 0, 7), (3, 3, 41, 0), (3, 3, 0, 1),
+                                      (4, 3, 0, 0), (4, 2, 0, 7), (5, 3, 0, 0), (5, 3, 0, 3), (6, 3, 0, 0),
+                                      (6, 2, 0, 1)]:
         r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
         assert r.describe()["kernel"] == "lanczos_stream"
-        if variant == 3:  # block-shared streamer in plain dispatch order
+        if variant == 3:  # block-shared streamer, one workgroup per (band, frame), plain dispatch order
             variant = 0
+            r.set_option("sweep", 0)
             r.set_option("xcd_order", 0)
+        elif variant == 4:  # one workgroup per (band, frame), XCD-aware order
+            variant = 0
+            r.set_option("sweep", 0)
+        elif variant in (5, 6):  # persistent XCD sweep with 1 or 2 workgroups per CU
+            r.set_option("sweep_wg", variant - 4)
+            variant = 0
         r.set_option("stream_variant", variant)
         r.set_option("prefetch", pd)
         r.set_option("lanes", lanes)
@@ -383,11 +392,11 @@ def test_tile_streamer_matches_oracle(cfg):
     frames[1, :, : sw // 3] = 255
     exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(2)]
     t = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    for k in ("walk", "a32", "d32", "up2", "u23", "l23"):
+    for k in ("walk", "a32", "d32", "d31", "ryx", "up2", "u23", "l23"):
         t.set_option(k, 0)
     assert t.describe()["kernel"] == "tile"
     r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-    for k in ("up2", "d32", "a32", "u23", "l23"):  # exact-ratio kernels off: the walker alone (their own tests below)
+    for k in ("up2", "d32", "d31", "ryx", "a32", "u23", "l23"):  # exact-ratio kernels off: the walker alone (their own tests below)
         r.set_option(k, 0)
     kern = r.describe()["kernel"]
     assert kern in ("walk", "tile")
@@ -400,7 +409,7 @@ def test_tile_streamer_matches_oracle(cfg):
     if kern == "walk":
         for bands in (1, 3, 7, dh):
             w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-            for k in ("up2", "d32", "a32", "u23", "l23"):
+            for k in ("up2", "d32", "d31", "ryx", "a32", "u23", "l23"):
                 w.set_option(k, 0)
             w.set_option("bands", bands)
             out = w.resize_tensor(src).cpu().numpy()
@@ -986,5 +995,180 @@ def test_linear_u23_matches_oracle(cfg):
     assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
     dst = torch.zeros((n, dh, dw + 2), dtype=torch.uint8, device=DEV)
     r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 2, dh * (dw + 2), dst.data_ptr())
+    torch.cuda.synchronize()
+    assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+
+
+AREA_INT_SHAPES = [
+    (3840, 2160, 1280, 720),   # 4K -> 720p, exactly 3:1 (12 source columns per thread)
+    (1920, 1080, 640, 360),
+    (1932, 1083, 644, 361),    # odd output height
+    (3840, 2160, 640, 720),    # 6:1 x 3:1
+    (3840, 2160, 1280, 1080),  # 3:1 x 2:1
+    (3840, 2160, 960, 540),    # 4:1 (16 columns per thread)
+]
+
+
+@pytest.mark.parametrize("shape", AREA_INT_SHAPES, ids=lambda s: "%dx%d_%dx%d" % s)
+def test_area_int_matches_oracle(shape):
+    """Area at integer ratios (area_int_kernel; 3:1 and 6:1 take 12-byte rows per thread) on noise,
+    flat and half-flat frames, dense and padded layouts, and the fused YUV420 launch at 3:1."""
+    sw, sh, dw, dh = shape
+    r = libiqo_amd.AreaResizer(sw, sh, dw, dh)
+    assert r.describe()["kernel"] == "area_int"
+    frames = _noise_batch(3, sw, sh, 900)
+    frames[1] = 255
+    frames[2, :, : sw // 2] = 0
+    exp = [ol.run_oracle("area", 0, sw, sh, dw, dh, 1, frames[f]) for f in range(3)]
+    out = r.resize_tensor(torch.from_numpy(frames).to(DEV)).cpu().numpy()
+    for f in range(3):
+        assert (out[f] == exp[f]).all(), (shape, f, np.argwhere(out[f] != exp[f])[:4].tolist())
+    # padded strides (still 4-byte aligned rows)
+    sst, dst_st = sw + 12, dw + 4
+    sbuf = torch.zeros((sh, sst), dtype=torch.uint8, device=DEV)
+    sbuf[:, :sw] = torch.from_numpy(frames[0]).to(DEV)
+    dbuf = torch.zeros((dh, dst_st), dtype=torch.uint8, device=DEV)
+    r.resize_device(1, sst, sh * sst, sbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :dw].cpu().numpy() == exp[0]).all()
+    if sw % 24 == 0 and sh % 2 == 0 and dw % 2 == 0 and dh % 2 == 0 and sw // dw == 3 and sh // dh == 3:
+        y = libiqo_amd.Yuv420Resizer("area", 0, sw, sh, dw, dh)
+        cw, ch = sw // 2, sh // 2
+        planes = [frames[0], ol.gen("noise", cw, ch, 5), ol.gen("noise", cw, ch, 6)]
+        src = torch.from_numpy(np.concatenate([p.ravel() for p in planes])[None]).to(DEV)
+        o, fused = y.resize_frames(src)
+        o = o.cpu().numpy()[0]
+        assert fused
+        assert (o[: dw * dh].reshape(dh, dw) == exp[0]).all()
+        ce = [ol.run_oracle("area", 0, cw, ch, dw // 2, dh // 2, 1, p) for p in planes[1:]]
+        cd = (dw // 2) * (dh // 2)
+        assert (o[dw * dh: dw * dh + cd].reshape(dh // 2, dw // 2) == ce[0]).all()
+        assert (o[dw * dh + cd:].reshape(dh // 2, dw // 2) == ce[1]).all()
+
+
+D31_SHAPES = [
+    ("lanczos", 3, 3840, 2160, 1280, 720, 1),    # 4K -> 720p: six waves per row (x0 of the last clamped)
+    ("lanczos", 3, 1920, 1080, 640, 360, 1),
+    ("lanczos", 2, 3840, 2160, 1280, 720, 1),    # Lanczos-2 tap structure
+    ("lanczos", 3, 1932, 1083, 644, 361, 1),     # odd output height
+    ("lanczos", 3, 336, 204, 112, 68, 1),        # one wave holding both edges
+    ("lanczos", 2, 192, 96, 64, 32, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", D31_SHAPES, ids=lambda c: "%s%d_%dx%d" % c[:4])
+def test_lanczos_d31_matches_oracle(cfg):
+    """Exact 3:1 Lanczos-2/3 downscale: lanczos_d31_kernel on every row and column (masked border
+    rows and columns divided in the kernel); equal to the oracle on noise, flat and half-flat
+    frames; equal to the general kernels (option d31 = 0); in several band splits, lane counts and
+    prefetch depths; in row bands through their source windows; with padded strides; and a
+    destination stride that is not 4-byte aligned (general kernels)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    n = 3
+    frames = _noise_batch(n, sw, sh, 3100)
+    frames[1] = 201
+    frames[2, :, : sw // 2] = 255
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert r.describe()["kernel"] == "lanczos_d31"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    w.set_option("d31", 0)
+    assert w.describe()["kernel"] in ("walk", "tile")
+    assert (w.resize_tensor(src).cpu().numpy() == out).all()
+    pds = (1, 5) if d == 3 else (1, 2, 4)
+    for opt, val in [("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 8), ("lanes", 62)] + \
+            [("ratio_prefetch", p) for p in pds]:
+        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option(opt, val)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
+    b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    b.set_option("ratio_prefetch", 3)  # not instantiated for this kernel: rejected, not ignored
+    with pytest.raises(libiqo_amd.IqoError):
+        b.resize_tensor(src)
+    # row bands through their source windows (odd band edges)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = [0, 3, dh // 3 + 1, dh // 2, dh - 5, dh]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    # padded strides (4-byte aligned rows): d31 again, nothing written past the row
+    sst, dst_st = sw + 4, dw + 4
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 9, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
+    assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
+    # destination stride not 4-byte aligned: the general kernels
+    dst = torch.zeros((n, dh, dw + 2), dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 2, dh * (dw + 2), dst.data_ptr())
+    torch.cuda.synchronize()
+    assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+
+
+RYX_SHAPES = [
+    ("lanczos", 3, 1920, 1080, 854, 480, 1),     # 1080p -> 480p: rows 9:4, columns 960:427
+    ("lanczos", 2, 1920, 1080, 854, 480, 1),
+    ("area", 0, 1920, 1080, 854, 480, 1),
+    ("lanczos", 3, 1920, 1080, 640, 480, 1),     # columns 3:1 (10 coefficient pairs)
+    ("lanczos", 3, 1280, 720, 570, 320, 1),
+    ("lanczos", 2, 720, 576, 1000, 256, 1),      # columns upscaled
+    ("area", 0, 720, 576, 360, 256, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", RYX_SHAPES, ids=lambda c: "%s%d_%dx%d_%dx%d" % c[:6])
+def test_ryx_matches_oracle(cfg):
+    """Exact vertical ratio with tabled columns (ryx_kernel): equal to the oracle on noise, flat and
+    half-flat frames, to the general kernels (option ryx = 0), over band splits, in row bands through
+    their source windows, with padded strides, and with an odd destination stride (general kernels)."""
+    m, d, sw, sh, dw, dh, px = cfg
+    n = 3
+    frames = _noise_batch(n, sw, sh, 4100)
+    frames[1] = 99
+    frames[2, :, sw // 3:] = 255
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, px, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    assert r.describe()["kernel"] == "ryx"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    w.set_option("ryx", 0)
+    assert w.describe()["kernel"] in ("walk", "tile")
+    assert (w.resize_tensor(src).cpu().numpy() == out).all()
+    for val in (1, 3, 7, dh):
+        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        b.set_option("bands", val)
+        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, val)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = [0, 3, dh // 3 + 1, dh // 2, dh - 5, dh]
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    sst, dst_st = sw + 8, dw + 6
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 9, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
+    assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
+    dst = torch.zeros((n, dh, dw + 1), dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 1, dh * (dw + 1), dst.data_ptr())
     torch.cuda.synchronize()
     assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg

@@ -17,7 +17,7 @@ import oracle_lib as ol
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
-KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4}
+KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6}
 
 
 @pytest.fixture(scope="module")
@@ -66,7 +66,12 @@ def _shapes():
            ("lanczos_u23", "lanczos", 3, 1280, 720, 1920, 1080),
            ("linear_u23", "linear", 0, 1280, 720, 1920, 1080),
            ("lanczos_up2", "lanczos", 3, 1920, 1080, 3840, 2160),
-           ("area_d32", "area", 0, 1920, 1080, 1280, 720), ("lanczos_up2", "lanczos", 2, 200, 60, 400, 120)]
+           ("area_d32", "area", 0, 1920, 1080, 1280, 720), ("lanczos_up2", "lanczos", 2, 200, 60, 400, 120),
+           ("lanczos_d31", "lanczos", 3, 3840, 2160, 1280, 720), ("lanczos_d31", "lanczos", 2, 1920, 1080, 640, 360),
+           ("lanczos_d31", "lanczos", 3, 1932, 1083, 644, 361),
+           ("ryx", "lanczos", 3, 1920, 1080, 854, 480), ("ryx", "lanczos", 2, 1920, 1080, 854, 480),
+           ("ryx", "area", 0, 1920, 1080, 854, 480), ("ryx", "lanczos", 3, 1920, 1080, 640, 480),
+           ("ryx", "lanczos", 3, 1280, 720, 570, 320), ("ryx", "area", 0, 720, 576, 360, 256)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -75,6 +80,10 @@ def _shapes():
         out.append(("linear_u23", "linear", 0, 8 * a, 2 * b, 12 * a, 3 * b))
         out.append(("area_d32", "area", 0, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_up2", "lanczos", rng.choice((2, 3)), 8 * a, b + 4, 16 * a, 2 * b + 8))
+        out.append(("lanczos_d31", "lanczos", rng.choice((2, 3)), 12 * a + 48, 3 * b + 24, 4 * a + 16, b + 8))
+        sw = 4 * rng.randint(20, 500)
+        out.append(("ryx", rng.choice(("lanczos", "area")), 3, sw, 9 * b + 36,
+                    2 * rng.randint(sw // 4 + 1, min(1024, sw) // 2), 4 * b + 16))
     return out
 
 
