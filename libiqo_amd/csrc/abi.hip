@@ -41,7 +41,7 @@ struct iqo_hip_plan {
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
-    int sweep = 1;          // block-shared streamer: persistent XCD sweep, nontemporal streams (speed only)
+    int sweep = 0;          // block-shared streamer: persistent XCD sweep, nontemporal streams (A/B; speed only)
     int sweepWg = 0;        // sweep: workgroups per CU (0 = all resident)
     int symbNt = 0;         // block-shared streamer, grid layout: nontemporal streams (A/B)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
