@@ -285,6 +285,29 @@ def test_256_frame_batch_bit_exact():
     torch.cuda.empty_cache()
 
 
+def test_1024_frame_batch_bit_exact():
+    """C5's whole batch (BASELINE.json configs[4]) in ONE launch on one GPU: 1024 C2 frames
+    (8.5 GB in, 2.1 GB out); frames 0, 511 and 1023 against the oracle, and the rest of the batch
+    against a second launch of the general kernel on a sample of frames."""
+    sw, sh, dw, dh = 3840, 2160, 1920, 1080
+    g = torch.Generator(device=DEV)
+    g.manual_seed(1024)
+    src = torch.randint(0, 256, (1024, sh, sw), dtype=torch.uint8, device=DEV, generator=g)
+    r = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh)
+    assert r.describe()["kernel"] == "lanczos_stream"
+    out = r.resize_tensor(src)
+    torch.cuda.synchronize()
+    for f in (0, 511, 1023):
+        exp = ol.run_oracle("lanczos", 3, sw, sh, dw, dh, 1, src[f].cpu().numpy())
+        assert (out[f].cpu().numpy() == exp).all(), f
+    gen = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh)
+    gen.set_option("force_general", 1)
+    pick = torch.tensor([1, 255, 256, 700, 1022], device=DEV)
+    assert torch.equal(gen.resize_tensor(src[pick].contiguous()), out[pick])
+    del src, out
+    torch.cuda.empty_cache()
+
+
 STREAM_SHAPES = [
     (3, 3840, 2160, 1920, 1080),  # C2: 4 waves x 60 lanes per row
     (2, 3840, 2160, 1920, 1080),
