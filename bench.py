@@ -38,9 +38,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level par
 
 CONFIGS = {
     # name: (method, degree, srcW, srcH, dstW, dstH, pxScale, default frames per GPU, label)
-    # C2: 128 frames per GPU = C5's share of its 1024-frame batch on 8 GPUs (per frame the same as
-    # 256 / 512 / 1024 frames per launch once batches rotate)
-    "c2": ("lanczos", 3, 3840, 2160, 1920, 1080, 1, 128, "C2 Lanczos-3 U8 1ch 3840x2160->1920x1080"),
+    # C2: 256 frames per launch, BASELINE.md section 4's minimum for C2 ("measure on device-resident
+    # batches: >= 256 frames for C2/C4"); the line also carries 128 frames (C5's per-GPU share of its
+    # 1024-frame batch on 8 GPUs) as batch_alt.  Per frame: 128 / 256 / 1024 frames = 2.22 / 2.15 /
+    # 2.08 us (profiles/r03/kernel_stats_c2_*frames.csv)
+    "c2": ("lanczos", 3, 3840, 2160, 1920, 1080, 1, 256, "C2 Lanczos-3 U8 1ch 3840x2160->1920x1080"),
     "c3": ("area", 0, 7680, 4320, 1920, 1080, 1, 64, "C3 Area U8 1ch 7680x4320->1920x1080"),
     "c4": ("linear", 0, 1920, 1080, 3840, 2160, 1, 256, "C4 Linear U8 1ch 1920x1080->3840x2160"),
     "c1": ("lanczos", 2, 640, 480, 320, 240, 1, 4096, "C1 Lanczos-2 U8 1ch 640x480->320x240"),
@@ -48,6 +50,10 @@ CONFIGS = {
     "g1": ("lanczos", 3, 1920, 1080, 1280, 720, 1, 128, "G1 Lanczos-3 U8 1ch 1920x1080->1280x720"),
     "g2": ("lanczos", 3, 1920, 1080, 3840, 2160, 1, 32, "G2 Lanczos-3 U8 1ch 1920x1080->3840x2160"),
     "g3": ("area", 0, 1920, 1080, 1280, 720, 1, 128, "G3 Area U8 1ch 1920x1080->1280x720"),
+    # video-ladder downscales past 2:1 (round 3 kernels): exact 3:1, exact 9:4 rows, Area 3:1
+    "g4": ("lanczos", 3, 3840, 2160, 1280, 720, 1, 128, "G4 Lanczos-3 U8 1ch 3840x2160->1280x720"),
+    "g5": ("lanczos", 3, 1920, 1080, 854, 480, 1, 256, "G5 Lanczos-3 U8 1ch 1920x1080->854x480"),
+    "g6": ("area", 0, 3840, 2160, 1280, 720, 1, 128, "G6 Area U8 1ch 3840x2160->1280x720"),
 }
 
 
@@ -224,8 +230,8 @@ def reuse_probe(step_batch, rot, dev, reps=10):
 
 def alt_batch(make_step, frames_alt, bytes_per_frame, dev, steps=20, warmup=3):
     """Kernel ms per launch at a second batch size, on rotated fresh batches like the headline
-    (BASELINE.md section 4 quotes C2 at >= 256 frames per launch; the headline uses C5's per-GPU
-    share of 128): same kernel, same plan, only the frame count differs."""
+    (the headline runs BASELINE.md section 4's 256 frames per launch; this is C5's per-GPU share of
+    128): same kernel, same plan, only the frame count differs."""
     import torch
 
     step, cleanup = make_step(frames_alt)
@@ -262,7 +268,7 @@ def main():
                     help="distinct device batches cycled through, one per step (0 = auto: >= 2.5 GB per cycle, "
                          "10x the Infinity Cache, so no step re-reads the previous steps' data from it)")
     ap.add_argument("--alt-frames", type=int, default=-1,
-                    help="also time this many frames per launch (rotated batches; -1 = 256 for c2, 0 = off)")
+                    help="also time this many frames per launch (rotated batches; -1 = 128 for c2, 0 = off)")
     ap.add_argument("--force-general", action="store_true")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="plan option (iqo_hip_plan_set_option), repeatable; speed-only A/B knobs")
@@ -433,7 +439,7 @@ def main():
         log("reuse probe: %s" % json.dumps(probe))
 
     alt = None
-    alt_frames = args.alt_frames if args.alt_frames >= 0 else (256 if args.config == "c2" else 0)
+    alt_frames = args.alt_frames if args.alt_frames >= 0 else (128 if args.config == "c2" else 0)
     if args.shard == "image" and alt_frames and alt_frames != frames:
         del src, dst
         torch.cuda.empty_cache()
@@ -476,12 +482,14 @@ def main():
     if rank == 0:
         value = out_px_step * args.steps / wall_max / 1e6
         achieved = bytes_launch / (kern_ms / 1e3) / 1e9
-        traffic = None
+        traffic, traffic_src = None, None
         try:
             with open(os.path.join(ROOT, "profiles", "pmc_%s.json" % args.config)) as f:
                 pmc = json.load(f)
             if pmc.get("frames") == frames and pmc.get("kernel") == kernel and args.shard == "image":
                 traffic = pmc.get("hbm_bytes_per_launch")
+                traffic_src = ("profiles/pmc_%s.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench command "
+                               "(scripts/gpu_ci.sh pmc, round %s), not measured in this run" % (args.config, pmc.get("round")))
         except Exception:
             pass
         par = ("image-sharded x%d (independent shards, no collective)" % world if args.shard == "image" else
@@ -508,7 +516,7 @@ def main():
                                ("device-resident batch" if args.shard == "image" else "row band of every frame")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel_ms_per_launch": round(kern_ms, 4),
+                         "traffic_source": traffic_src, "kernel_ms_per_launch": round(kern_ms, 4),
                          "algorithmic_bytes_per_launch": int(bytes_launch)},
             "cpu_baseline": cpu,
             "parity": parity,

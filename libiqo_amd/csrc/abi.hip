@@ -41,9 +41,6 @@ struct iqo_hip_plan {
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
-    int sweep = 0;          // block-shared streamer: persistent XCD sweep, nontemporal streams (A/B; speed only)
-    int sweepWg = 0;        // sweep: workgroups per CU (0 = all resident)
-    int symbNt = 0;         // block-shared streamer, grid layout: nontemporal streams (A/B)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
@@ -530,9 +527,6 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
         l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
     l.np = h->lanes;
     l.xcd = h->xcdOrder;
-    l.sweep = h->sweep;
-    l.sweepWg = h->sweepWg;
-    l.nt = h->symbNt;
     return l;
 }
 
@@ -1035,20 +1029,6 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "ring_pack")) {  // block-shared Lanczos streamer: packed ring rows (speed only)
         h->ringPack = value != 0;
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "sweep")) {  // block-shared Lanczos streamer: persistent XCD sweep (A/B)
-        h->sweep = value != 0;
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "symb_nt")) {  // block-shared streamer, grid layout: nontemporal streams (A/B)
-        h->symbNt = value != 0;
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "sweep_wg")) {  // sweep: workgroups per CU (0 = all resident)
-        if (value < 0 || value > 8)
-            return IQO_HIP_EINVAL;
-        h->sweepWg = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "xcd_order")) {  // block-shared Lanczos streamer workgroup order (A/B)

@@ -47,23 +47,12 @@ __device__ __forceinline__ unsigned xcd_spread(unsigned L, unsigned n)
     return xcd < r ? xcd * (q + 1u) + idx : r * (q + 1u) + (xcd - r) * q + idx;
 }
 
-#ifndef IQO_LIN_LOAD_NT
-#define IQO_LIN_LOAD_NT 0  // Linear 2x streamer: default-policy source loads (fresh data C4: 1 % faster
-                           // than nontemporal; the Area streamer keeps nontemporal: 9 % faster on C3)
-#endif
-
-// 16-byte streaming load (source pixels are read once per band): nontemporal hint unless
-// IQO_AREA_LOAD_NT = 0.
-#ifndef IQO_AREA_LOAD_NT
-#define IQO_AREA_LOAD_NT 1
-#endif
+// 16-byte streaming load with the nontemporal hint (source pixels are read once per band; Area
+// streamer: 9 % faster on C3 than the default policy.  The Linear 2x streamer keeps the default
+// policy: 1 % faster on C4)
 __device__ __forceinline__ uint4 load16_nt(const uint8_t *p)
 {
-#if IQO_AREA_LOAD_NT
     u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-#else
-    u32x4 v = *reinterpret_cast<const u32x4 *>(p);
-#endif
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -302,40 +291,25 @@ struct TileArgs {
     unsigned nTiles;    // nTx * nTy * frames (flat grid)
 };
 
-#ifndef IQO_TILE_XCD
-#define IQO_TILE_XCD 1  // XCD-aware flat tile order (0: 3-D grid in dispatch order, A/B only)
-#endif
-
 template <int NP, bool LZ>
 __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t tile_lds[];
     const TileDev &t = a.t;
     const int tid = static_cast<int>(threadIdx.x);
-#if IQO_TILE_XCD
     // Workgroups are dispatched round-robin over the 8 XCDs (flat id L goes to XCD L mod 8), and
     // each XCD has its own L2.  Give XCD x a contiguous range of tiles, row tiles fastest: the
     // tiles resident on one XCD at a time are vertical (and horizontal) neighbours, so the halo
-    // rows / columns they share are fetched from HBM once and hit that XCD's L2 afterwards.
+    // rows / columns they share are fetched from HBM once and hit that XCD's L2 afterwards
+    // (round 2: column tiles fastest and plain dispatch order both slower, profiles/r02/tile_xcd_ab.txt).
     int tileX, tileY, frame;
     {
         const unsigned lg = xcd_spread(blockIdx.x, a.nTiles);
-#if IQO_TILE_XCD == 2  // A/B: column tiles fastest
-        const unsigned rest = lg / static_cast<unsigned>(a.nTx);
-        tileX = static_cast<int>(lg - rest * static_cast<unsigned>(a.nTx));
-        frame = static_cast<int>(rest / static_cast<unsigned>(a.nTy));
-        tileY = static_cast<int>(rest - static_cast<unsigned>(frame) * static_cast<unsigned>(a.nTy));
-#else
         const unsigned rest = lg / static_cast<unsigned>(a.nTy);
         tileY = static_cast<int>(lg - rest * static_cast<unsigned>(a.nTy));
         frame = static_cast<int>(rest / static_cast<unsigned>(a.nTx));
         tileX = static_cast<int>(rest - static_cast<unsigned>(frame) * static_cast<unsigned>(a.nTx));
-#endif
     }
-#else
-    const int tileX = static_cast<int>(blockIdx.x), tileY = static_cast<int>(blockIdx.y);
-    const int frame = static_cast<int>(blockIdx.z);
-#endif
     const int y0 = a.rowBegin + tileY * t.TH;
     const int nRows = min(t.TH, a.rowEnd - y0);
     // LDS: work rows [TH][pitchDw] | row records [TH] | tap records [TH][nYp] (coefficient, LDS
@@ -461,9 +435,6 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
             const uint8_t *colL = srcL + (max(cb, 0) - colStart);
             const uint2 *tj = taps + j * t.nYp;
             uint32_t acc0 = 0, acc1 = 0, acc2 = 0, acc3 = 0;
-#ifdef IQO_TILE_UNROLL2
-#pragma unroll 2
-#endif
             for (int i = 0; i < t.nYp; i += 2) {
                 const uint4 c2 = *reinterpret_cast<const uint4 *>(tj + i);  // (coef, offset) x 2
                 const u32x2 v0 = *reinterpret_cast<const u32x2 *>(colL + c2.y);
@@ -573,9 +544,6 @@ struct LanczosArgs {
     int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
     int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
     int lastLanes;           // block-shared streamer: lanes of the last DMA chunk (0 = all 64)
-    int sweep;               // block-shared streamer: persistent XCD sweep over (frame, band) items
-    int frames;              // items = frames x bands (sweep)
-    int noAlt;               // every band walks top-down (sweep: nontemporal streams prefer it)
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -814,51 +782,32 @@ __global__ __launch_bounds__(256, 3) void lanczos_stream_kernel(LanczosArgs a)
 //    (> np+1) load nothing (out-of-range offsets) and store nothing.  Rows past the band's last
 //    needed source row are loaded out of range too (no HBM traffic).
 
-// 16-byte-per-lane LDS-DMA of one source row into LDS bytes [lds, lds + 1024) of this wave.
-// M0 is saved and restored inside the statement (it is compiler-reserved).
-#ifndef IQO_SYMB_PRO_NT
-#define IQO_SYMB_PRO_NT 0  // window prologue loads: default policy (the neighbouring band reads the same halo rows)
-#endif
-#ifndef IQO_DMA_NT
-#define IQO_DMA_NT 0  // LDS-DMA source reads with the default cache policy (fresh data, C2: 2.7 % faster than
-                     // nontemporal: the halo rows neighbouring bands share stay in L2)
-#endif
-__device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff, bool nt = IQO_DMA_NT)
+// 16-byte-per-lane LDS-DMA of one source row into LDS bytes [lds, lds + 1024) of this wave, with
+// the default cache policy (fresh data, C2: 2.7 % faster than nontemporal -- the halo rows that
+// neighbouring bands share stay in L2).  M0 is saved and restored inside the statement (it is
+// compiler-reserved).
+__device__ __forceinline__ void dma_row(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff)
 {
     uint32_t keep;
-    if (nt)
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
-                     : "memory");
-    else
-        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-                     : "=&s"(keep)
-                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
-                     : "memory");
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory");
 }
 
 // dma_row for the lanes of `mask` only (masked-off lanes write nothing to LDS): the last chunk of a
 // ring row DMAs just the bytes the row needs, so the ring rows can be packed tighter than 1 KiB
 __device__ __forceinline__ void dma_row_masked(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff,
-                                               uint64_t mask, bool nt = IQO_DMA_NT)
+                                               uint64_t mask)
 {
     uint32_t keep;
     uint64_t save;
-    if (nt)
-        asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %3, %4, %5 offen nt lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
-                     : "=&s"(keep), "=&s"(save)
-                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
-                     : "memory");
-    else
-        asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                     "buffer_load_dwordx4 %3, %4, %5 offen lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
-                     : "=&s"(keep), "=&s"(save)
-                     : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
-                     : "memory");
+    asm volatile("s_mov_b64 %1, exec\n\ts_mov_b64 exec, %6\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %3, %4, %5 offen lds\n\ts_mov_b32 m0, %0\n\ts_mov_b64 exec, %1"
+                 : "=&s"(keep), "=&s"(save)
+                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff), "s"(mask)
+                 : "memory");
 }
 
 template <int N>
@@ -988,7 +937,7 @@ __device__ __forceinline__ void lanczos_sym_kernel_body(const LanczosArgs &a, co
         uint4 w0[NY - 2];
 #pragma unroll
         for (int t = 0; t < NY - 2; ++t) {
-            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), IQO_SYMB_PRO_NT ? 2 : 0);
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), 0);
             w0[t] = make_uint4(q.x, q.y, q.z, q.w);
         }
 #pragma unroll
@@ -1109,46 +1058,36 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 // row before it is refilled.  Waves with fewer chunks than CPW DMA into a sink so the vm-counter
 // pattern is the same in every wave.
 
-template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, bool NT = false>
-#ifndef IQO_SWEEP_NTL
-#define IQO_SWEEP_NTL 1  // sweep: nontemporal LDS-DMA source loads and window prologue loads
+#ifndef IQO_SYMB_VORDER
+#define IQO_SYMB_VORDER 0  // vertical pass instruction order (A/B)
 #endif
-#ifndef IQO_SWEEP_NTS
-#define IQO_SWEEP_NTS 1  // sweep: nontemporal output stores
+#ifndef IQO_SYMB_EXP
+#define IQO_SYMB_EXP 0  // timing experiments in variant builds (wrong output): 1 no vertical MACs,
+                        // 2 half the horizontal dots, 3 / 4 dot2 / dot4 in place of the MACs
 #endif
-#ifndef IQO_SWEEP_ALT
-#define IQO_SWEEP_ALT 0  // sweep: odd bands walk bottom-up as in the grid layout
-#endif
-#ifndef IQO_SWEEP_EDGE_DEF
-#define IQO_SWEEP_EDGE_DEF 1  // nontemporal modes: the edge waves store with the default policy
-#endif
-#ifndef IQO_SYMB_WAVES_PER_EU
-#define IQO_SYMB_WAVES_PER_EU 4
-#endif
-#ifndef IQO_SYMB_DPPDOT
-#define IQO_SYMB_DPPDOT 1  // neighbour pairs through DPP-modified v_dot2c (C2: ~1% faster)
-#endif
-#ifndef IQO_SYMB_LA
-#define IQO_SYMB_LA 1  // LDS look-ahead in the block-shared streamer (C2: ~1% faster)
-#endif
-#ifndef IQO_SYMB_NT_STORE
-#define IQO_SYMB_NT_STORE 0
-#endif
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 #ifndef IQO_SYMB_EDGE_BATCH
 #define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (C2: 64 -> 16 cuts write traffic +4.5% -> +2%)
 #endif
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
 __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
 {
     constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
     static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
-    static_assert(K >= 2 && CPW >= 1, "ring depth");
-    constexpr int WAIT = 1 + (K - 2) * (2 * CPW + 1);  // vm ops issued after this wave's DMA(i)
-#if IQO_SYMB_LA
+    static_assert(K >= 3 && CPW >= 1, "ring depth (the LDS look-ahead needs K >= 3)");
     // LDS look-ahead: iteration i reads the ring slot of iteration i+1 (its latency hides behind
-    // iteration i's arithmetic), so it waits for DMA(i+1): one fewer DMA iteration in flight
-    static_assert(K >= 3, "look-ahead needs K >= 3");
-    constexpr int WAITLA = 1 + (K - 3) * (2 * CPW + 1);
-#endif
+    // iteration i's arithmetic), so it waits for DMA(i+1): after this wave's DMA(i+1) come the
+    // store of iteration i-K+2 and the 2*CPW DMAs + 1 store of each of iterations i+2 .. i+K-2
+    constexpr int WAIT = 1 + (K - 2) * (2 * CPW + 1);   // prologue: DMA(0) retired
+    constexpr int WAITLA = 1 + (K - 3) * (2 * CPW + 1); // iteration i: DMA(i+1) retired
+    // K == H: the ring period equals the window period, so every slot index in the unrolled body
+    // is a compile-time constant (immediate LDS offsets, no per-row slot arithmetic)
+    constexpr bool CSLOT = K == H;
     constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
     constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
     static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
@@ -1199,17 +1138,15 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     // same time (both at their start or both at their end) and the second read hits the
     // Infinity Cache instead of HBM.  The window arithmetic is symmetric, so only the row order
     // changes: walk index t of iteration i is source row rowAt(i, t).
-    const int dir = ((band & 1) && !(dbg & 32) && (!a.noAlt || IQO_SWEEP_ALT)) ? -1 : 1;
+    const int dir = ((band & 1) && !(dbg & 32)) ? -1 : 1;
     const int rFirst = 2 * y0 + L.offY;                 // first source row the band reads
     const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;  // last source row the band reads
     const int nRows = y1 - y0;
     const uint32_t bias = opaque(1u << 19);            // rounding bias (VOP3P src2 of the first dot)
-#if IQO_SYMB_DPPDOT
-    uint32_t cvx[NX / 2];  // X coefficient pairs in VGPRs (VOP2 DPP needs a VGPR src1)
+    uint32_t cvx[NX / 2];  // X coefficient pairs in VGPRs (the VOP2 DPP dot needs a VGPR src1)
 #pragma unroll
     for (int p = 0; p < NX / 2; ++p)
         cvx[p] = opaque(L.cxo[p]);
-#endif
 
     // shared LDS ring: iteration i's two walk rows live in slot i mod K; chunk c (1 KiB of
     // source columns [1024c, 1024c + 1024) at LDS column 16 + 1024c) is DMA'd by wave c mod wpr
@@ -1219,28 +1156,34 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     auto row_soff = [&](int r) { return (r >= rFirst && r <= rLast) ? (r - srcRow0) * srcSt : 0x7ff00000; };
     // iteration i (output row y0 + i, or y1 - 1 - i walking up) brings walk rows NY-2 and NY-1
     auto rowAt = [&](int i, int t) { return dir > 0 ? rFirst + 2 * i + t : rLast - 2 * i - t; };
-    auto dma_iter = [&](int i) {
-        const uint32_t s = ldsBase + static_cast<uint32_t>((i % K) * slotBytes);
-        const int r = rowAt(i, NY - 2);
+    // the DMA rows of iteration j are linear in j and inside [rFirst, rLast] exactly when j < nRows
+    // (the last iteration brings the band's last two rows), so their offsets are one running
+    // value instead of two range checks per row
+    const int dmaSoff0 = (rowAt(0, NY - 2) - srcRow0) * srcSt, dmaStep = 2 * dir * srcSt, dmaNext = dir * srcSt;
+    auto dma_iter = [&](int j, int slot) {
+        const uint32_t s = ldsBase + static_cast<uint32_t>(slot * slotBytes);
+        const bool in = j < nRows;
+        const int so0 = in ? dmaSoff0 + j * dmaStep : 0x7ff00000;
+        const int so1 = in ? dmaSoff0 + j * dmaStep + dmaNext : 0x7ff00000;
 #pragma unroll
-        for (int j = 0; j < CPW; ++j) {
-            const int c = wcol + j * wpr;
+        for (int jj = 0; jj < CPW; ++jj) {
+            const int c = wcol + jj * wpr;
             const bool real = c < a.chunks;  // uniform; otherwise a same-count DMA into the sink
             const int col = 1024 * c + 16 * lane;
             const int v = (real && col < L.srcW && !(dbg & 2)) ? col : 0x7ff00000;
             const uint32_t d0 = real ? s + 16 + 1024 * c : ldsBase + sinkLds;
             const uint32_t d1 = real ? d0 + rowPitch : d0;
             if (real && c == a.chunks - 1 && lastLanes < 64) {  // uniform
-                dma_row_masked(d0, v, srcR, row_soff(r), lastMask, (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
-                dma_row_masked(d1, v, srcR, row_soff(r + dir), lastMask, (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
+                dma_row_masked(d0, v, srcR, so0, lastMask);
+                dma_row_masked(d1, v, srcR, so1, lastMask);
             } else {
-                dma_row(d0, v, srcR, row_soff(r), (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
-                dma_row(d1, v, srcR, row_soff(r + dir), (NT && IQO_SWEEP_NTL) || IQO_DMA_NT);
+                dma_row(d0, v, srcR, so0);
+                dma_row(d1, v, srcR, so1);
             }
         }
     };
-    auto read_iter = [&](int i, uint4 &r0, uint4 &r1) {
-        const uint8_t *p = ringLane + (i % K) * slotBytes;
+    auto read_iter = [&](int slot, uint4 &r0, uint4 &r1) {
+        const uint8_t *p = ringLane + slot * slotBytes;
         r0 = *reinterpret_cast<const uint4 *>(p);
         r1 = *reinterpret_cast<const uint4 *>(p + rowPitch);
     };
@@ -1287,11 +1230,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     // iteration i brings the last two (t = NY-2, NY-1)
     uint32_t win[NY][8];
     {
-        // walk rows 0 .. NY-3 of iteration 0 go straight to VGPRs (window slots 0 .. NY-3)
+        // walk rows 0 .. NY-3 of iteration 0 go straight to VGPRs (window slots 0 .. NY-3); the
+        // default cache policy: the neighbouring band reads the same halo rows
         uint4 w0[NY - 2];
 #pragma unroll
         for (int t = 0; t < NY - 2; ++t) {
-            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), ((NT && IQO_SWEEP_NTL) || IQO_SYMB_PRO_NT) ? 2 : 0);
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcR, svoff, row_soff(rowAt(0, t)), 0);
             w0[t] = make_uint4(q.x, q.y, q.z, q.w);
         }
 #pragma unroll
@@ -1305,25 +1249,22 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     // iteration on the vm counter sees the steady-state order DMA(j), S(j-K+1)
 #pragma unroll
     for (int j = 0; j < K - 1; ++j) {
-        dma_iter(j);
+        dma_iter(j, j);
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstR, 0x7ff00000, 0, 0);
     }
 
-#if IQO_SYMB_LA
     uint4 n0, n1;  // this iteration's two new rows (read from LDS one iteration ahead)
     wait_vmcnt<WAIT>();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     read_iter(0, n0, n1);
-#endif
     auto row = [&](auto uc, int base) {
         constexpr int v = decltype(uc)::value;
         const int i = base + v;  // iteration = output row y0 + i
         if (i >= nRows)
             return;  // past the band end (uniform)
         const int yy = dir > 0 ? y0 + i : y1 - 1 - i;
-#if IQO_SYMB_LA
         // this wave's DMA(i+1) retired (WAITLA younger vm ops); the barrier publishes slot i+1
         // and retires every wave's reads of slot i-1, which DMA(i+K-1) refills
         wait_vmcnt<WAITLA>();
@@ -1331,26 +1272,12 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         uint4 m0, m1;
-        read_iter(i + 1, m0, m1);
-        dma_iter(i + K - 1);
-#else
-        // this wave's DMA(i) retired: after it come the store of iteration i-K+1 and the 2*CPW
-        // DMAs + 1 store of each of iterations i-K+2 .. i-1; then the workgroup barrier makes
-        // every wave's chunks of iteration i visible and retires all reads of slot (i-1) mod K
-        wait_vmcnt<WAIT>();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        uint4 n0, n1;
-        read_iter(i, n0, n1);
-        dma_iter(i + K - 1);  // into slot (i-1) mod K, read in iteration i-1
-#endif
+        read_iter(CSLOT ? (v + 1) % K : (i + 1) % K, m0, m1);
+        dma_iter(i + K - 1, CSLOT ? (v + K - 1) % K : (i + K - 1) % K);
         unpack_odd(n0, win[(2 * v + NY - 2) % NY]);
         unpack_odd(n1, win[(2 * v + NY - 1) % NY]);
-#if IQO_SYMB_LA
         n0 = m0;
         n1 = m1;
-#endif
 
         // vertical: pair p = slots (2v + p, 2v + NY - 1 - p) mod NY
         uint32_t acc[8];
@@ -1359,6 +1286,50 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             const uint32_t p0 = win[(2 * v) % NY][c] + win[(2 * v + NY - 1) % NY][c];
             acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
         }
+#if IQO_SYMB_EXP == 1  // timing experiment (variant build, wrong output): pair sums only, no MACs
+#pragma unroll
+        for (int p = 1; p < H; ++p)
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c] += win[(2 * v + p) % NY][c];
+#elif IQO_SYMB_EXP == 3  // timing experiment: v_dot2c in place of v_pk_mad_u16
+#pragma unroll
+        for (int p = 1; p < H; ++p)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
+                acc[c] = static_cast<uint32_t>(sdot2(pp, L.cy[p], static_cast<int>(acc[c])));
+            }
+#elif IQO_SYMB_EXP == 4  // timing experiment: v_dot4 in place of v_pk_mad_u16
+#pragma unroll
+        for (int p = 1; p < H; ++p)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
+                asm("v_dot4_i32_i8 %0, %1, %2, %0" : "+v"(acc[c]) : "s"(L.cy[p]), "v"(pp));
+            }
+#else
+        {
+#if IQO_SYMB_VORDER == 1
+        // all pair sums of a tap pair first, then its 8 MACs (no add -> MAC back-to-back dependency)
+#pragma unroll
+        for (int p = 1; p < H; ++p) {
+            uint32_t pp[8];
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                pp[c] = opaque(win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c]);
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c] = pk_mad(pp[c], L.cy[p], acc[c]);
+        }
+#elif IQO_SYMB_VORDER == 2
+        // packed 16-bit pair sums (v_pk_add_u16) feeding the MACs
+#pragma unroll
+        for (int p = 1; p < H; ++p)
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c] = pk_mad(pk_add16(win[(2 * v + p) % NY][c], win[(2 * v + NY - 1 - p) % NY][c]), L.cy[p], acc[c]);
+#else
 #pragma unroll
         for (int p = 1; p < H; ++p)
 #pragma unroll
@@ -1366,6 +1337,9 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                 const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
                 acc[c] = pk_mad(pp, L.cy[p], acc[c]);
             }
+#endif
+        }
+#endif
         if ((yy < L.mainBeginY || yy >= L.mainEndY) && !(dbg & 8)) {
             // border row (uniform, rare): rows outside the image were read as zero
             const bool top = yy < L.mainBeginY;
@@ -1377,16 +1351,13 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                 acc[c] = ydiv2(acc[c], m, sh);
         }
 
+        // horizontal: the neighbour pairs enter the dot products through the DPP source modifier
+        // of v_dot2c_i32_i16 (no separate v_mov_dpp); each output starts with an own pair (VOP3P
+        // form, the bias VGPR as src2).  s_nop 1: DPP reads of VGPRs the vertical pass just wrote.
         int sum[8];
-#if IQO_SYMB_DPPDOT
-        // neighbour pairs enter the dot products through the DPP source modifier of
-        // v_dot2c_i32_i16 (no separate v_mov_dpp); each output starts with an own pair (VOP3P form,
-        // the bias VGPR as src2).  s_nop 1: DPP reads of VGPRs the vertical pass just wrote.
         asm volatile("s_nop 1" ::: "memory");
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            constexpr int dummy = 0;
-            (void)dummy;
             int pFirst = -1;  // first tap whose pair is this lane's own
 #pragma unroll
             for (int p = 0; p < NX / 2; ++p) {
@@ -1400,7 +1371,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 #pragma unroll
             for (int p = 0; p < NX / 2; ++p) {
                 const int j = k + p + JLO;
-                if (p == pFirst)
+                if (p == pFirst || (IQO_SYMB_EXP == 2 && (p & 1)))  // experiment 2: half the taps (timing only)
                     continue;
                 if (j <= 0)
                     asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
@@ -1413,49 +1384,13 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             }
             sum[k] = sacc;
         }
-#else
-        // Q_j for j in [JLO, JHI): own pairs 1..8, neighbours' by DPP
-        uint32_t q[JHI - JLO];
-#pragma unroll
-        for (int j = JLO; j < JHI; ++j) {
-            if (j <= 0)
-                q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
-                    static_cast<int>(acc[j + 7]), 0x138 /* wave_shr:1 */, 0xf, 0xf, true));
-            else if (j >= 9)
-                q[j - JLO] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(
-                    static_cast<int>(acc[j - 9]), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
-            else
-                q[j - JLO] = acc[j - 1];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            int sacc;  // VOP3P form: the bias VGPR is src2, no copy into the accumulator
-            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[0]), "v"(q[k]), "v"(bias));
-#pragma unroll
-            for (int p = 1; p < NX / 2; ++p)
-                sacc = sdot2(q[k + p], L.cxo[p], sacc);
-            sum[k] = sacc;
-        }
-#endif
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-#ifdef IQO_VARIANT_DEBUG
-        if (dbg & 64) {  // timing experiment (wrong output): the row's bytes as 16 B per even lane
-            const int st16 = (lane & 1) ? 0x7ff00000 : stoff;
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o.x, o.y, o.x, o.y}, dstR, st16, (yy - a.io.dstRow0) * dstSt, 0);
-        } else
-#endif
-        // nontemporal stores leave L2 at once; the edge waves' lines get their border bytes rewritten
-        // up to EB rows later (flush_edges), so those waves keep the default policy and the two
-        // writes of a line merge in L2 instead of reaching HBM as two partial-line writes
-        if ((NT && IQO_SWEEP_NTS && !(IQO_SWEEP_EDGE_DEF && (edgeL || edgeR))) || IQO_SYMB_NT_STORE)
-            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 2);
-        else
-            __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
         if (edgeL || edgeR) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
-            // LDS; every 64 rows and at the band end one pass divides them, one row per lane
+            // LDS; every EB rows and at the band end one pass divides them, one row per lane
             const int slot = i & (EB - 1);
             if (edgeL && laneL)
                 edgeSum[0][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
@@ -1472,37 +1407,9 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
-template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, int MODE = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WAVES_PER_EU))) void lanczos_symb_kernel(LanczosArgs a)
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lanczos_symb_kernel(LanczosArgs a)
 {
-    // MODE 2 is the sweep layout (nontemporal), MODE 0 / 1 the (band, frame) grid with default /
-    // nontemporal streams (prep_lanczos picks the instantiation): one body per instantiation
-    constexpr bool NT = MODE >= 1;
-    if constexpr (MODE == 2) {
-        // Persistent XCD sweep (option "sweep", default for large batches): the (frame, band) items
-        // in frame-major order are cut into 8 contiguous ranges, XCD x (workgroups b with b mod 8 = x
-        // under the round-robin placement; speed only) takes range x, and its workgroups take the
-        // items j, j + G/8, ... of it.  At any time an XCD reads a compact window of its own frames
-        // (one band per workgroup, bands of ~34 rows), and loads and stores are nontemporal: on fresh
-        // data this memory stream sustains ~6.0-6.3 TB/s against 5.2-5.4 for one workgroup per band
-        // scattered over the batch (scripts/ubench/c2mem.hip, profiles/r03/ubench_c2mem_*.txt).
-        const unsigned G = gridDim.x, n = static_cast<unsigned>(a.bands) * static_cast<unsigned>(a.frames);
-        unsigned lo = 0, hi = n, j = blockIdx.x, step = G;
-        if (G % 8u == 0) {
-            const unsigned x = blockIdx.x & 7u, q = n >> 3, r = n & 7u;
-            lo = x * q + min(x, r);
-            hi = lo + q + (x < r ? 1u : 0u);
-            j = blockIdx.x >> 3;
-            step = G >> 3;
-        }
-        for (unsigned i = lo + j; i < hi; i += step) {
-            const unsigned frame = i / static_cast<unsigned>(a.bands);
-            lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE, NT>(a, i - frame * static_cast<unsigned>(a.bands), frame);
-            // every wave's reads of the ring and edge slots are done before the next item's DMAs
-            __syncthreads();
-        }
-        return;
-    } else {
     unsigned bx = blockIdx.x, by = blockIdx.y;
     if (a.xcd) {
         // XCD-aware order (speed only): the band workgroups of one frame go to one XCD, so the
@@ -1513,8 +1420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IQO_SYMB_WA
         by = lg / bands;
         bx = lg - by * bands;
     }
-    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE, NT>(a, bx, by);
-    }
+    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, bx, by);
 }
 
 
@@ -2013,7 +1919,7 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
 
     auto load_row = [&](int r) -> u32x2 {
         return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff, r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000,
-                                                    IQO_LIN_LOAD_NT ? 2 /* nt */ : 0);
+                                                    0);  // default policy: 1 % faster than nt on C4
     };
     auto unpack = [&](u32x2 v, uint32_t (&P)[5]) {
         const uint32_t left = static_cast<uint32_t>(
@@ -2143,18 +2049,6 @@ struct Up2Args {
     unsigned nWaves;
 };
 
-#ifndef IQO_UP2_NT_STORE
-#define IQO_UP2_NT_STORE 1  // nontemporal 16-B stores (fresh data G2: 0.088 vs 0.1015 ms)
-#endif
-#ifndef IQO_D32_NT_STORE
-#define IQO_D32_NT_STORE 0
-#endif
-#ifndef IQO_A32_LOAD_NT
-#define IQO_A32_LOAD_NT 0
-#endif
-#ifndef IQO_A32_NT_STORE
-#define IQO_A32_NT_STORE 0
-#endif
 template <int NT>
 __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
 {
@@ -2216,7 +2110,7 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     };
     auto store_row = [&](u32x4 o, int voffs, int y, bool ok) {
         __builtin_amdgcn_raw_buffer_store_b128(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0,
-                                               IQO_UP2_NT_STORE ? 2 /* nt */ : 0);
+                                               2 /* nt: fresh data G2 0.088 vs 0.1015 ms */);
     };
     // masked border row (uniform, rare): work = int16(n * 64 / deno)
     auto border_row = [&](uint32_t (&W)[4], int y) {
@@ -2459,7 +2353,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         P[5] = __builtin_amdgcn_perm(0u, v.z, 0x0c030c02u);  // (cb+10, cb+11)
     };
     auto store_row = [&](u32x2 o, int voffs, int y, bool ok) {
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, IQO_D32_NT_STORE ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
     };
     // horizontal pass of one output row from the lane's six work pairs; the edge lane parks its sums
     auto emit = [&](const uint32_t (&W)[6], int y, int slot) {
@@ -3422,7 +3316,7 @@ __global__ __launch_bounds__(256) void area_d32_kernel(A32Args a)
     auto load_row = [&](int r) -> u32x3 {
         const int rc = min(max(r, srcRow0), srcLast);
         return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (r <= rLast ? (rc - srcRow0) * srcSt : OOB), 0,
-                                                    IQO_A32_LOAD_NT ? 2 /* nt */ : 0);
+                                                    0);
     };
     auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
         P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);
@@ -3442,7 +3336,7 @@ __global__ __launch_bounds__(256) void area_d32_kernel(A32Args a)
                         udot2(E[2], d.cx[1], b));
         o.y = pack23_hi(pack23_lo(udot2(E[3], d.cx[0], b), udot2(O7, d.cx[1], b)), udot2(O9, d.cx[0], b),
                         udot2(E[5], d.cx[1], b));
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff + (y >= y0 && y < y1 ? (y - dstRow0) * dstSt : OOB), 0, IQO_A32_NT_STORE ? 2 : 0);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff + (y >= y0 && y < y1 ? (y - dstRow0) * dstSt : OOB), 0, 0);
     };
 
     u32x3 pre[PD][3];
@@ -3500,7 +3394,7 @@ template <int NY, int NX, int OFFX, bool ONE>
 struct SymbY {
     static __device__ __forceinline__ void run(const LanczosArgs &a, unsigned bx, unsigned by)
     {
-        lanczos_symb_kernel_body<NY, NX, OFFX, 4, 1, ONE>(a, bx, by);
+        lanczos_symb_kernel_body<NY, NX, OFFX, NY / 2, 1, ONE>(a, bx, by);  // ring depth = window period (prep_lanczos)
     }
 };
 template <int NY, int NX, int OFFX, bool ONE>
@@ -3643,11 +3537,7 @@ hipError_t launch_tile(const TileDev &t, const Io &io, int rowBegin, int rowEnd,
                static_cast<unsigned>(nTiles)};
     const size_t lds = static_cast<size_t>(t.TH) * (static_cast<size_t>(t.pitchDw) * 4 + 16 + static_cast<size_t>(t.nYp) * 8) +
                        4u * static_cast<size_t>(t.CT) + static_cast<size_t>(t.srcRows) * t.spitch;
-#if IQO_TILE_XCD
     dim3 grid(static_cast<unsigned>(nTiles));
-#else
-    dim3 grid(static_cast<unsigned>(nTx), static_cast<unsigned>(nTy), static_cast<unsigned>(io.frames));
-#endif
 #define IQO_TILE(NP_)                                                                                \
     case NP_:                                                                                        \
         kern = t.lanczos ? reinterpret_cast<const void *>(tile_kernel<NP_, true>)                    \
@@ -4094,22 +3984,22 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int chunks = (rowNeed - 16 + 1023) / 1024;
     const int lastLanes = (rowNeed - 16 - 1024 * (chunks - 1)) / 16;
     const int cpw = (chunks + wpr - 1) / wpr;
-    const int rowPitch = l.ringPack ? rowNeed : 16 + 1024 * chunks;
     const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
-    // persistent XCD sweep (kernels.hip lanczos_symb_kernel): one-wave-row-per-band layouts only
-    const bool sweep = shared && l.sweep != 0;
+    // block-shared ring depth: prefetch 1-2 -> 3, 3 (default) -> the window period NY/2 (4 for
+    // Lanczos-2, 5 for Lanczos-3: every ring slot index is then a compile-time constant; C2 x256
+    // 0.5226 vs 0.532 ms at depth 4), 4 -> 5.  Depth 5 packs the ring rows to the bytes they need
+    // so that four 4-wave workgroups still fit a CU's LDS.
+    const int K = pd <= 2 ? 3 : pd == 3 ? (l.NY == 10 ? 5 : 4) : 5;
+    const bool pack = l.ringPack || (shared && K == 5);
+    const int rowPitch = pack ? rowNeed : 16 + 1024 * chunks;
     if (shared) {
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
-        const int K = pd <= 2 ? 3 : pd == 3 ? 4 : 5;
         ldsBytes = K * 2 * rowPitch + 2 * IQO_SYMB_EDGE_BATCH * 16 + (cpw * wpr > chunks ? 1024 : 0);
         block = 64 * wpr;
-#define IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, M_)                                                         \
-    (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 1, ONE_, M_>)                \
-              : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 2, ONE_, M_>))
 #define IQO_SYMB_K(NY_, NX_, OX_, K_, ONE_)                                                             \
-    (sweep ? IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, 2)                                                     \
-           : l.nt ? IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, 1) : IQO_SYMB_M(NY_, NX_, OX_, K_, ONE_, 0))
+    (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 1, ONE_>)                  \
+              : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 2, ONE_>))
 #define IQO_SYMB(NY_, NX_, OX_, ONE_)                                                                   \
     (K == 3 ? IQO_SYMB_K(NY_, NX_, OX_, 3, ONE_) : K == 4 ? IQO_SYMB_K(NY_, NX_, OX_, 4, ONE_)          \
             : IQO_SYMB_K(NY_, NX_, OX_, 5, ONE_))
@@ -4121,7 +4011,6 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB
 #undef IQO_SYMB_K
-#undef IQO_SYMB_M
     } else if (l.sym) {
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         if (l.NY == 10 && one)
@@ -4145,30 +4034,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
                : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 2>)
                          : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 3>);
     }
-    int sweepGrid = 0;
-    if (sweep) {
-        // resident workgroups (optionally fewer per CU), one band of ~34 rows per workgroup and at
-        // least one item per workgroup: 32 bands per frame on large batches
-        int cus = 256;
-        {
-            int dev = 0;
-            hipDeviceProp_t prop;
-            if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                cus = prop.multiProcessorCount;
-        }
-        const int residentWg = std::max(1, resident_waves(kern, block, ldsBytes) / wpr);
-        const int wgs = l.sweepWg > 0 ? std::min(residentWg, l.sweepWg * cus) : residentWg;
-        if (bands <= 0)
-            bands = std::min(std::max(32, (wgs + io.frames - 1) / io.frames), std::max(1, rows / 8));
-        bands = max(1, min(bands, rows));
-        const int rpb0 = (rows + bands - 1) / bands;
-        bands = (rows + rpb0 - 1) / rpb0;
-        const int64_t items = static_cast<int64_t>(bands) * io.frames;
-        int64_t g = std::min<int64_t>(wgs, items);
-        if (g >= 8)
-            g -= g % 8;
-        sweepGrid = static_cast<int>(g);
-    } else if (bands <= 0) {
+    if (bands <= 0) {
         const int resident = resident_waves(kern, block, ldsBytes);
         if (shared && l.rounds >= 0) {
             // block-shared ring: about `rounds` rounds of resident workgroups (default 6), bands of
@@ -4187,7 +4053,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
     a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd,
-                    l.ringPack ? lastLanes : 64, sweep ? 1 : 0, io.frames, sweep ? 1 : 0};
+                    pack ? lastLanes : 64};
     // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -4198,13 +4064,12 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
-    P->grid = sweep    ? dim3(static_cast<unsigned>(sweepGrid))
-              : shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
+    P->grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
                        : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
     P->block = block;
     P->lds = ldsBytes;
     P->kern = kern;
-    P->kind = shared ? (sweep ? 3 : 1) : (l.sym ? 2 : 0);
+    P->kind = shared ? 1 : (l.sym ? 2 : 0);
     P->pd = pd;
     return hipSuccess;
 }
@@ -4341,7 +4206,6 @@ hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const Lanc
     Prep<LanczosArgs> py, pu, pv;
     hipError_t e;
     LanczosDev lyGrid = ly;
-    lyGrid.sweep = 0;  // the fused launch needs the (band, frame) grid of every plane
     if ((e = prep_lanczos(lyGrid, ioY, 0, ly.dstH, 0, &py)) != hipSuccess ||
         (e = prep_lanczos(lc, ioU, 0, lc.dstH, 0, &pu)) != hipSuccess ||
         (e = prep_lanczos(lc, ioV, 0, lc.dstH, 0, &pv)) != hipSuccess)

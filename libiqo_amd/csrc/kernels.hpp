@@ -187,10 +187,6 @@ struct LanczosDev {
     int ringPack;                // block-shared streamer: ring rows packed to the bytes they need
     int rounds;                  // block-shared streamer: target rounds of resident workgroups for the
                                  // auto band count (0 = default 6, -1 = one-round makespan model)
-    int sweep;                   // block-shared streamer: 1 = persistent XCD sweep with nontemporal
-                                 // streams (default), 0 = one workgroup per (band, frame)
-    int sweepWg;                 // sweep: workgroups per CU (0 = as many as are resident)
-    int nt;                      // grid layout: nontemporal source loads and output stores
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,

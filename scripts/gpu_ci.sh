@@ -28,15 +28,15 @@ fi
 if want prof; then
   cd /tmp || exit 1
   for c in ${PROF_CFGS:-c2 c3 c4 g1 g2 g3}; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o run -- python3 "$ROOT/bench.py" --config $c --steps 10 --warmup 2 --no-cpu --no-verify --no-probe > "$OUT/prof_$c.log" 2>&1 || { echo "prof $c failed"; tail -20 "$OUT/prof_$c.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o run -- python3 "$ROOT/bench.py" --config $c --steps 10 --warmup 2 --no-cpu --no-verify --no-probe --alt-frames 0 > "$OUT/prof_$c.log" 2>&1 || { echo "prof $c failed"; tail -20 "$OUT/prof_$c.log"; exit 1; }
   done
   cd "$ROOT" || exit 1
 fi
 if want pmc; then
   cd /tmp || exit 1
   for c in ${PMC_CFGS:-c2 c3 c4 g1}; do
-    timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify --no-probe > "$OUT/pmc_fetch_$c.log" 2>&1 || { echo "pmc fetch $c failed"; tail -20 "$OUT/pmc_fetch_$c.log"; exit 1; }
-    timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify --no-probe > "$OUT/pmc_write_$c.log" 2>&1 || { echo "pmc write $c failed"; tail -20 "$OUT/pmc_write_$c.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify --no-probe --alt-frames 0 > "$OUT/pmc_fetch_$c.log" 2>&1 || { echo "pmc fetch $c failed"; tail -20 "$OUT/pmc_fetch_$c.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --config $c --steps 3 --warmup 1 --no-cpu --no-verify --no-probe --alt-frames 0 > "$OUT/pmc_write_$c.log" 2>&1 || { echo "pmc write $c failed"; tail -20 "$OUT/pmc_write_$c.log"; exit 1; }
   done
   cd "$ROOT" || exit 1
 fi

@@ -329,22 +329,18 @@ def test_stream_variants_agree_with_oracle(shape):
     src = torch.from_numpy(frames).to(DEV)
     exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 1, frames[f]) for f in range(2)]
     for variant, pd, lanes, bands in [(0, 1, 0, 0), (0, 2, 0, 7), (0, 3, 0, 0), (0, 2, 62, 3), (0, 3, 33, 0),
-                                      (0, 3, 0, 1), (1, 3, 0, 0), (1, 1, 0, 5), (2, 3, 0, 0), (2, 1, 0, 5),
-                                      (2, 2, 40, 0), (3, 3, 0, 0), (3, 2, 0, 7), (3, 3, 41, 0), (3, 3, 0, 1),
-                                      (4, 3, 0, 0), (4, 2, 0, 7), (5, 3, 0, 0), (5, 3, 0, 3), (6, 3, 0, 0),
-                                      (6, 2, 0, 1)]:
+                                      (0, 3, 0, 1), (0, 4, 0, 0), (0, 4, 0, 7), (1, 3, 0, 0), (1, 1, 0, 5),
+                                      (2, 3, 0, 0), (2, 1, 0, 5), (2, 2, 40, 0), (3, 3, 0, 0), (3, 2, 0, 7),
+                                      (3, 3, 41, 0), (3, 3, 0, 1), (4, 4, 0, 0), (4, 4, 0, 7), (4, 3, 0, 3),
+                                      (4, 2, 0, 1), (4, 4, 33, 1)]:
         r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
         assert r.describe()["kernel"] == "lanczos_stream"
-        if variant == 3:  # block-shared streamer, one workgroup per (band, frame), plain dispatch order
+        if variant == 3:  # block-shared streamer in plain dispatch order
             variant = 0
-            r.set_option("sweep", 0)
             r.set_option("xcd_order", 0)
-        elif variant == 4:  # one workgroup per (band, frame), XCD-aware order
+        elif variant == 4:  # packed ring rows (prefetch 4: ring depth 5 = the Lanczos-3 window period)
             variant = 0
-            r.set_option("sweep", 0)
-        elif variant in (5, 6):  # persistent XCD sweep with 1 or 2 workgroups per CU
-            r.set_option("sweep_wg", variant - 4)
-            variant = 0
+            r.set_option("ring_pack", 1)
         r.set_option("stream_variant", variant)
         r.set_option("prefetch", pd)
         r.set_option("lanes", lanes)
