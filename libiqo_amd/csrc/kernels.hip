@@ -2751,14 +2751,19 @@ struct RyxArgs {
 };
 
 template <bool LZ, int P, int Q, int T, int OFF, int NP, int PD>
-__global__ __launch_bounds__(512) void ryx_kernel(RyxArgs a)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryx_kernel(RyxArgs a)
 {
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
     constexpr int NW = (SPAN + P - 1) / P * P;    // register window rows (whole groups of P)
     constexpr int U = NW / P;                     // groups per unrolled trip (window slots repeat)
+    constexpr int UQ = U * Q;                     // output rows per trip
     constexpr int OOB = 0x7ff00000;
     constexpr int PADB = 2 * kRyxPadK;            // work-row byte padding left of column 0
     static_assert(U % PD == 0, "prefetch slots repeat within a trip");
+    static_assert(UQ % 2 == 0, "work-row buffer parity is static within a trip");
+    // the next row's vertical pass overlaps this row's LDS reads when the read registers fit
+    // beside the window (NP 10 would spill at 4 waves per SIMD)
+    constexpr bool PIPE = NP <= 8;
     const RyxDev &d = a.d;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int t = static_cast<int>(threadIdx.x);
@@ -2781,7 +2786,11 @@ __global__ __launch_bounds__(512) void ryx_kernel(RyxArgs a)
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
-    const int voff = 4 * t < d.srcW ? 4 * t : OOB;
+#ifndef IQO_RYX_EXP
+#define IQO_RYX_EXP 0  // timing experiments (variant builds, wrong output): 1 no source loads, 2 no stores,
+                       // 3 no barriers
+#endif
+    const int voff = 4 * t < d.srcW && IQO_RYX_EXP != 1 ? 4 * t : OOB;
 
     // work rows: two buffers of (pad + srcW + pad) u16, zero padding written once
     const int pitch = PADB + 2 * d.srcW + PADB;
@@ -2807,17 +2816,22 @@ __global__ __launch_bounds__(512) void ryx_kernel(RyxArgs a)
         for (int q = 0; q < NP; ++q)
             cf[k][q] = d.colCoef[x * NP + q];
     }
-    const int stoff = x0 < d.dstW ? x0 : OOB;  // dstW is even (launch_ryx)
+    // interior Lanczos columns divide by 2^20 (magic_x: m = 2^31, shift 19), which is one
+    // saturating pack of both columns; only the few border columns take the exact division
+    const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
+    const int stoff = x0 < d.dstW && IQO_RYX_EXP != 2 ? x0 : OOB;  // dstW is even (launch_ryx)
 
-    // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1
+    // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1.
+    // Rows outside the image load as zero (the reference's masked border sums); rows past the
+    // band's last window are not loaded.  Rows outside the call's source window (band windows) can
+    // only be rows no stored output reads, and read as zero (out-of-range offsets).
     const int rBase = P * mLo + OFF;
     const int rLast = P * (mLo + nG - 1) + OFF + SPAN - 1;
-    const int srcLast = a.io.srcRowEnd - 1;
+    const int qLo = max(0, -rBase), qHi = min(d.srcH - 1, rLast) - rBase;
+    const int rowOff0 = (rBase - srcRow0) * srcSt;
     auto load_row = [&](int q) -> uint32_t {
-        const int r = rBase + q;
-        const int rc = min(max(r, srcRow0), srcLast);
-        const bool in = r >= 0 && r < d.srcH && r <= rLast;
-        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
+        const bool in = static_cast<unsigned>(q - qLo) <= static_cast<unsigned>(qHi - qLo);
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? rowOff0 + q * srcSt : OOB), 0, 0);
     };
     auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
         W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
@@ -2835,67 +2849,131 @@ __global__ __launch_bounds__(512) void ryx_kernel(RyxArgs a)
         for (int i = 0; i < P; ++i)
             pre[v][i] = load_row(SPAN - P + P * v + i);
 
-    int row = 0;  // output rows emitted by this workgroup: work buffer parity
+    // group g (window slot base v = g mod U) brings its P new rows into the window and issues the
+    // loads of group g + PD
+    auto enter_group = [&](auto vc, int g) {
+        constexpr int v = decltype(vc)::value;
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            widen(pre[v % PD][i], R[(P * v + SPAN - P + i) % NW]);
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            pre[v % PD][i] = load_row(SPAN - P + P * (g + PD) + i);
+    };
+    // vertical pass of output row Q (mLo + g) + j into work buffer B: phase j's taps from window
+    // row floor(P j / Q) (scalar loads of the splats), packed MACs, 16-bit wrap; masked Lanczos
+    // border rows are divided in place
+    // (the splats arrive in cy, loaded before the barrier that precedes the pass: scalar loads
+    // share the lgkm counter with the LDS reads, and waiting for them after the barrier would
+    // also wait for the row's LDS reads)
+    auto coefs = [&](auto jc, uint32_t (&cy)[T]) {
+        constexpr int j = decltype(jc)::value;
+#pragma unroll
+        for (int k = 0; k < T; ++k)
+            cy[k] = static_cast<uint32_t>(sld(d.rowCoef, j * T + k));
+    };
+    auto vertical = [&](auto vc, auto jc, auto bc, int g, const uint32_t (&cy)[T]) {
+        constexpr int v = decltype(vc)::value, j = decltype(jc)::value, B = decltype(bc)::value;
+        constexpr int S0 = (P * j) / Q;
+        const int y = Q * (mLo + g) + j;
+        uint32_t W[2] = {0u, 0u};
+#pragma unroll
+        for (int k = 0; k < T; ++k) {
+            W[0] = pk_mad(R[(P * v + S0 + k) % NW][0], cy[k], W[0]);
+            W[1] = pk_mad(R[(P * v + S0 + k) % NW][1], cy[k], W[1]);
+        }
+        if (LZ && (y < d.m0 || y >= d.m1)) {
+            // masked border row (uniform, rare): rows outside the image read as zero
+            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
+            W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
+            W[1] = ydiv2(W[1], d.yM[side][i], d.yS[side][i]);
+        }
+        if (4 * t < d.srcW)
+            *reinterpret_cast<uint2 *>(lds + B * pitch + PADB + 8 * t) = make_uint2(W[0], W[1]);
+    };
+
+    // prologue: group 0's rows, output row 0 into buffer 0
+    enter_group(std::integral_constant<int, 0>{}, 0);
+    {
+        uint32_t cy0[T];
+        coefs(std::integral_constant<int, 0>{}, cy0);
+        vertical(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0,
+                 cy0);
+    }
+
+    // Row r of a trip (group base + r / Q, phase r % Q): the barrier publishes its work row
+    // (written one iteration earlier); its NP-pair windows are read from LDS, and while those
+    // reads are in flight the thread computes the vertical pass of row r + 1 into the other buffer
+    // (every read of that buffer, row r - 1, completed before the barrier); then the dots
+    // (without PIPE the next row's vertical pass comes after the dots).
     for (int base = 0; base < nG; base += U) {
-        static_for<U>([&](auto vc) {
-            constexpr int v = decltype(vc)::value;
+        static_for<UQ>([&](auto rc) {
+            constexpr int r = decltype(rc)::value;
+            constexpr int v = r / Q, j = r % Q, B = r & 1;
             const int g = base + v;
             if (g >= nG)
                 return;  // whole workgroup
-#pragma unroll
-            for (int i = 0; i < P; ++i)
-                widen(pre[v % PD][i], R[(P * v + SPAN - P + i) % NW]);
-#pragma unroll
-            for (int i = 0; i < P; ++i)
-                pre[v % PD][i] = load_row(SPAN - P + P * (g + PD) + i);
-            static_for<Q>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                constexpr int S0 = (P * j) / Q;  // window row of tap 0
-                const int y = Q * (mLo + g) + j;
-                // vertical: phase j's taps (scalar loads of the splats)
-                uint32_t W[2] = {0u, 0u};
-#pragma unroll
-                for (int k = 0; k < T; ++k) {
-                    const uint32_t c = static_cast<uint32_t>(sld(d.rowCoef, j * T + k));
-                    W[0] = pk_mad(R[(P * v + S0 + k) % NW][0], c, W[0]);
-                    W[1] = pk_mad(R[(P * v + S0 + k) % NW][1], c, W[1]);
-                }
-                if (LZ && (y < d.m0 || y >= d.m1)) {
-                    // masked border row (uniform, rare): rows outside the image read as zero
-                    const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
-                    W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
-                    W[1] = ydiv2(W[1], d.yM[side][i], d.yS[side][i]);
-                }
-                uint8_t *wr = lds + (row & 1) * pitch;
-                if (4 * t < d.srcW)
-                    *reinterpret_cast<uint2 *>(wr + PADB + 8 * t) = make_uint2(W[0], W[1]);
+            constexpr int rn = (r + 1) % UQ, vn = rn / Q, jn = rn % Q;
+            uint32_t cyn[T];  // the next row's splats, complete at the barrier
+            coefs(std::integral_constant<int, jn>{}, cyn);
+            if (IQO_RYX_EXP != 3)  // experiment 3: no barrier (timing only)
                 __syncthreads();
-                // horizontal: the thread's two columns
+            const uint8_t *wr = lds + B * pitch;
+            uint32_t w[2][NP];
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int q = 0; q < NP; ++q)
+                    w[k][q] = reinterpret_cast<const uint32_t *>(wr + aoff[k])[q];
+            // the next row's vertical pass (the next trip's first row after the trip's last)
+            auto next_vertical = [&]() {
+                const int gn = base + (r + 1) / Q;
+                if (gn < nG) {
+                    if constexpr (jn == 0)
+                        enter_group(std::integral_constant<int, vn>{}, gn);
+                    vertical(std::integral_constant<int, vn>{}, std::integral_constant<int, jn>{},
+                             std::integral_constant<int, B ^ 1>{}, gn, cyn);
+                }
+            };
+            if constexpr (PIPE)
+                next_vertical();
+            // horizontal: the thread's two columns
+            const int y = Q * (mLo + g) + j;
+            uint32_t packed;
+            if constexpr (LZ) {
+                int acc[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    acc[k] = 1 << 19;
+#pragma unroll
+                    for (int q = 0; q < NP; ++q)
+                        acc[k] = sdot2(w[k][q], cf[k][q], acc[k]);
+                }
+                if (edgeT) {
+                    const uint32_t o0 = min(__umulhi(static_cast<uint32_t>(max(acc[0], 0)), mm[0]) >> sh[0], 255u);
+                    const uint32_t o1 = min(__umulhi(static_cast<uint32_t>(max(acc[1], 0)), mm[1]) >> sh[1], 255u);
+                    packed = opaque(o0) | (opaque(o1) << 8);
+                } else {
+                    packed = pack_lo(acc[0], acc[1]);  // sat_u8(acc >> 20) of both columns
+                }
+            } else {
                 int o[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
-                    const uint32_t *w = reinterpret_cast<const uint32_t *>(wr + aoff[k]);
-                    if constexpr (LZ) {
-                        int acc = 1 << 19;
+                    uint32_t acc = 1u << 22;
 #pragma unroll
-                        for (int q = 0; q < NP; ++q)
-                            acc = sdot2(w[q], cf[k][q], acc);
-                        o[k] = static_cast<int>(min(__umulhi(static_cast<uint32_t>(max(acc, 0)), mm[k]) >> sh[k], 255u));
-                    } else {
-                        uint32_t acc = 1u << 22;
-#pragma unroll
-                        for (int q = 0; q < NP; ++q)
-                            acc = udot2(w[q], cf[k][q], acc);
-                        const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
-                        o[k] = u > 255 ? 255 : u;
-                    }
+                    for (int q = 0; q < NP; ++q)
+                        acc = udot2(w[k][q], cf[k][q], acc);
+                    const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
+                    o[k] = u > 255 ? 255 : u;
                 }
-                const bool ok = y >= y0 && y < y1;
-                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(opaque(static_cast<uint32_t>(o[0])) |
-                                                                            (opaque(static_cast<uint32_t>(o[1])) << 8)),
-                                                      dstR, stoff + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
-                ++row;
-            });
+                packed = opaque(static_cast<uint32_t>(o[0])) | (opaque(static_cast<uint32_t>(o[1])) << 8);
+            }
+            const bool ok = y >= y0 && y < y1;
+            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(packed), dstR,
+                                                  stoff + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+            if constexpr (!PIPE)
+                next_vertical();
         });
     }
 }
