@@ -54,6 +54,9 @@ CONFIGS = {
     "g4": ("lanczos", 3, 3840, 2160, 1280, 720, 1, 128, "G4 Lanczos-3 U8 1ch 3840x2160->1280x720"),
     "g5": ("lanczos", 3, 1920, 1080, 854, 480, 1, 256, "G5 Lanczos-3 U8 1ch 1920x1080->854x480"),
     "g6": ("area", 0, 3840, 2160, 1280, 720, 1, 128, "G6 Area U8 1ch 3840x2160->1280x720"),
+    # narrow frames (frame-stacked streamer): the C1 I420 chroma plane size, single channel
+    "n1": ("lanczos", 2, 320, 240, 160, 120, 1, 16384, "N1 Lanczos-2 U8 1ch 320x240->160x120"),
+    "n2": ("lanczos", 3, 640, 360, 320, 180, 1, 4096, "N2 Lanczos-3 U8 1ch 640x360->320x180"),
 }
 
 

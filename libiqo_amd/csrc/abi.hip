@@ -27,6 +27,16 @@ using iqo_amd::Plan;
 struct iqo_hip_plan {
     Plan p;
     int device = 0;
+    // Device tables (general / tile / walker / ratio-Y kernels) are staged into one host blob at
+    // plan creation and uploaded by ONE allocation and copy the first time a launch needs them:
+    // the specialised kernels take their coefficients as kernel arguments, so a plan that only
+    // ever runs them costs no device allocation (the reference benchmark constructs its resizers
+    // inside the timed loop, benchmark/benchmark.cpp:206-229).
+    std::vector<uint8_t> blob;
+    std::vector<std::pair<void **, size_t>> blobPtrs;  // member pointer, byte offset in the blob
+    uint8_t *dBlob = nullptr;
+    bool tablesUp = false;
+    std::mutex tablesMu;
     int4 *dX = nullptr, *dY = nullptr, *dChunks = nullptr;
     int *dTabX = nullptr, *dTabY = nullptr;
     int nChunks = 0, ldsInts = 0;
@@ -40,6 +50,7 @@ struct iqo_hip_plan {
     int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
+    int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
@@ -115,6 +126,7 @@ private:
 // is never torn down (the HIP runtime may already be gone at static destruction).
 constexpr int kHostBands = 8;      // output-row bands of the host-pointer pipeline
 constexpr int kHostBandRows = 64;  // ... each at least this tall
+constexpr size_t kHostPipeMinBytes = size_t(4) << 20;  // smaller frames: one band (API latency dominates)
 
 struct HostStage {
     int device = 0;
@@ -242,14 +254,34 @@ bool is_gfx950(int dev)
 }
 
 template <typename T>
-int upload(T **dptr, const T *src, size_t n)
+int upload(iqo_hip_plan *h, T **dptr, const T *src, size_t n)
 {
-    if (n == 0)
-        n = 1;
-    if (hipMalloc(reinterpret_cast<void **>(dptr), n * sizeof(T)) != hipSuccess)
-        return IQO_HIP_ENOMEM;
-    if (src && hipMemcpy(*dptr, src, n * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-        return IQO_HIP_EHIP;
+    // stage into the plan's blob (256-B aligned sections); ensure_tables uploads it on first use
+    const size_t off = (h->blob.size() + 255) & ~static_cast<size_t>(255);
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    h->blob.resize(off + bytes, 0);
+    if (src && n)
+        std::memcpy(h->blob.data() + off, src, n * sizeof(T));
+    h->blobPtrs.emplace_back(reinterpret_cast<void **>(dptr), off);
+    *dptr = nullptr;
+    return IQO_HIP_OK;
+}
+
+// One allocation + one copy of every staged table, then the table pointers point into it.
+int ensure_tables(iqo_hip_plan *h)
+{
+    std::lock_guard<std::mutex> lock(h->tablesMu);
+    if (h->tablesUp)
+        return IQO_HIP_OK;
+    if (!h->blob.empty()) {
+        if (hipMalloc(reinterpret_cast<void **>(&h->dBlob), h->blob.size()) != hipSuccess)
+            return IQO_HIP_ENOMEM;
+        if (hipMemcpy(h->dBlob, h->blob.data(), h->blob.size(), hipMemcpyHostToDevice) != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
+    for (const auto &pr : h->blobPtrs)
+        *pr.first = h->dBlob + pr.second;
+    h->tablesUp = true;
     return IQO_HIP_OK;
 }
 
@@ -303,24 +335,7 @@ int build_chunks(const Plan &p, std::vector<int4> *chunks, int *ldsInts)
 
 void free_plan(iqo_hip_plan *h)
 {
-    (void)hipFree(h->dX);
-    (void)hipFree(h->dY);
-    (void)hipFree(h->dChunks);
-    (void)hipFree(h->dTabX);
-    (void)hipFree(h->dTabY);
-    (void)hipFree(h->dTRows);
-    (void)hipFree(h->dTCols);
-    (void)hipFree(h->dTSpans);
-    (void)hipFree(h->dTRowTap);
-    (void)hipFree(h->dTColCoef);
-    (void)hipFree(h->dTColA);
-    (void)hipFree(h->dRyxRowCoef);
-    (void)hipFree(h->dRyxColCoef);
-    (void)hipFree(h->dRyxCols);
-    (void)hipFree(h->dWSpans);
-    (void)hipFree(h->dWRowTap);
-    (void)hipFree(h->dWRows);
-    (void)hipFree(h->dWSegs);
+    (void)hipFree(h->dBlob);
     delete h;
 }
 
@@ -380,13 +395,13 @@ int upload_tile(iqo_hip_plan *h)
         for (size_t i = 0; i < wr.size(); ++i)
             wr[i] = make_int4(h->wt.rows[i].lo, h->wt.rows[i].hi, h->wt.rows[i].hiSlot, h->wt.rows[i].deno);
         const std::vector<uint32_t> &wt = h->wt.rowTap;
-        int rc = upload(&h->dWSpans, ws.data(), ws.size());
+        int rc = upload(h, &h->dWSpans, ws.data(), ws.size());
         if (!rc)
-            rc = upload(&h->dWRows, wr.data(), wr.size());
+            rc = upload(h, &h->dWRows, wr.data(), wr.size());
         if (!rc)
-            rc = upload(&h->dWRowTap, wt.data(), wt.size());
+            rc = upload(h, &h->dWRowTap, wt.data(), wt.size());
         if (!rc)
-            rc = upload(&h->dWSegs, sg.data(), sg.size());
+            rc = upload(h, &h->dWSegs, sg.data(), sg.size());
         if (rc)
             return rc;
     }
@@ -399,11 +414,11 @@ int upload_tile(iqo_hip_plan *h)
         std::vector<int4> rc(h->ryx.cols.size() / 4);
         for (size_t i = 0; i < rc.size(); ++i)
             rc[i] = make_int4(h->ryx.cols[4 * i], h->ryx.cols[4 * i + 1], h->ryx.cols[4 * i + 2], 0);
-        int rc2 = upload(&h->dRyxRowCoef, h->ryx.rowCoef.data(), h->ryx.rowCoef.size());
+        int rc2 = upload(h, &h->dRyxRowCoef, h->ryx.rowCoef.data(), h->ryx.rowCoef.size());
         if (!rc2)
-            rc2 = upload(&h->dRyxColCoef, h->ryx.colCoef.data(), h->ryx.colCoef.size());
+            rc2 = upload(h, &h->dRyxColCoef, h->ryx.colCoef.data(), h->ryx.colCoef.size());
         if (!rc2)
-            rc2 = upload(&h->dRyxCols, rc.data(), rc.size());
+            rc2 = upload(h, &h->dRyxCols, rc.data(), rc.size());
         if (rc2)
             return rc2;
     }
@@ -419,10 +434,10 @@ int upload_tile(iqo_hip_plan *h)
             rowTap[y * t.nYp + i] = make_uint2(t.rowCoef[y * t.nYp + i], static_cast<uint32_t>(row));
         }
     int rc;
-    if ((rc = upload(&h->dTRows, rows.data(), rows.size())) || (rc = upload(&h->dTCols, cols.data(), cols.size())) ||
-        (rc = upload(&h->dTSpans, spans.data(), spans.size())) ||
-        (rc = upload(&h->dTRowTap, rowTap.data(), rowTap.size())) ||
-        (rc = upload(&h->dTColCoef, coefT.data(), coefT.size())) || (rc = upload(&h->dTColA, colA.data(), colA.size())))
+    if ((rc = upload(h, &h->dTRows, rows.data(), rows.size())) || (rc = upload(h, &h->dTCols, cols.data(), cols.size())) ||
+        (rc = upload(h, &h->dTSpans, spans.data(), spans.size())) ||
+        (rc = upload(h, &h->dTRowTap, rowTap.data(), rowTap.size())) ||
+        (rc = upload(h, &h->dTColCoef, coefT.data(), coefT.size())) || (rc = upload(h, &h->dTColA, colA.data(), colA.size())))
         return rc;
     return IQO_HIP_OK;
 }
@@ -461,10 +476,10 @@ int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t d
     h->nChunks = static_cast<int>(chunks.size());
     iqo_amd::build_tile_tables(h->p, &h->tt);
     std::vector<int4> xr = coord_records(h->p.x), yr = coord_records(h->p.y);
-    if ((rc = upload(&h->dX, xr.data(), xr.size())) || (rc = upload(&h->dY, yr.data(), yr.size())) ||
-        (rc = upload(&h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
-        (rc = upload(&h->dTabY, h->p.y.table.data(), h->p.y.table.size())) ||
-        (rc = upload(&h->dChunks, chunks.data(), chunks.size())) || (rc = upload_tile(h))) {
+    if ((rc = upload(h, &h->dX, xr.data(), xr.size())) || (rc = upload(h, &h->dY, yr.data(), yr.size())) ||
+        (rc = upload(h, &h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
+        (rc = upload(h, &h->dTabY, h->p.y.table.data(), h->p.y.table.size())) ||
+        (rc = upload(h, &h->dChunks, chunks.data(), chunks.size())) || (rc = upload_tile(h))) {
         free_plan(h);
         return rc;
     }
@@ -520,6 +535,7 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.prefetch = h->prefetch;
     l.ringPack = h->ringPack;
     l.rounds = h->rounds;
+    l.stack = h->stack;
     l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
     l.NX = f.NX;
     l.offXO = f.offXO;
@@ -886,6 +902,12 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
         return IQO_HIP_ENODEV;
 
     const int kernel = kernel_for_layout(h, src, srcSt, srcFrameSt, dst, dstSt, dstFrameSt);
+    if (kernel == IQO_KERNEL_TILE || kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_RYX ||
+        kernel == IQO_KERNEL_GENERAL) {
+        const int rc = ensure_tables(h);
+        if (rc)
+            return rc;
+    }
 
     const int rb = static_cast<int>(r0), re = static_cast<int>(r0 + rows);
     // Frames per launch: at most 65535 (grid y).  The option "chunk_frames" splits further into
@@ -1025,6 +1047,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < -1 || value > 64)
             return IQO_HIP_EINVAL;
         h->rounds = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "stack")) {  // narrow frames side by side in one workgroup (speed only):
+        if (value < 0 || value > 2)        // 0 off, 1 where a frame fills <= 1/2 wave, 2 from 2 frames
+            return IQO_HIP_EINVAL;
+        h->stack = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "ring_pack")) {  // block-shared Lanczos streamer: packed ring rows (speed only)
@@ -1183,7 +1211,7 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
         return IQO_HIP_ENOMEM;
 
     const int dstH = p.dstH;
-    const int bands = std::max(1, std::min(kHostBands, dstH / kHostBandRows));
+    const int bands = sBytes < kHostPipeMinBytes ? 1 : std::max(1, std::min(kHostBands, dstH / kHostBandRows));
     auto bandRow = [&](int b) { return static_cast<int>(static_cast<int64_t>(dstH) * b / bands); };
     int rowsUp = 0;  // source rows [0, rowsUp) are queued for upload
     for (int b = 0; b < bands; ++b) {

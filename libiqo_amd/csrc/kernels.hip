@@ -544,6 +544,7 @@ struct LanczosArgs {
     int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
     int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
     int lastLanes;           // block-shared streamer: lanes of the last DMA chunk (0 = all 64)
+    int fpw, frames;         // frame-stacked streamer: frames per workgroup, frames in the launch
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -1423,6 +1424,270 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
     lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, bx, by);
 }
 
+
+// ================================================================ frame-stacked streamer (narrow frames)
+//
+// The block-shared streamer gives a row of srcW source columns srcW / 16 producing lanes; a
+// 640-column frame (C1: 640x480 -> 320x240) fills 40 of a wave's 64 lanes.  Here FPW frames sit
+// side by side in the lanes of one 2-wave workgroup: virtual lane v (wave w, lane l: v = 62 w + l;
+// each wave's lanes 0 and 63 are its halo) holds, for v = 1 + (np + 1) F + k, frame F's source
+// columns [16 k, 16 k + 16) (k < np), and the virtual lanes between frames (k = np) and at both
+// ends are zero -- exactly the zero columns outside the image that give the reference's masked
+// border sums, so every frame's arithmetic is the block-shared streamer's unchanged (3 frames of
+// 40 lanes = 120 of the 128 lanes produce).  Each ring row holds the FPW frames' rows at LDS bytes
+// 16 v, DMA'd one frame row per instruction (lanes past the row masked).  Requirements (host):
+// srcW = 2 dstW, srcW % 16 == 0, np = srcW / 16, FPW (np + 1) + 1 <= 126.
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void lanczos_stack_kernel(LanczosArgs a)
+{
+    constexpr int H = NY / 2;
+    static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
+    static_assert(K == H && CPW >= 1, "ring depth = window period");
+    constexpr int WAIT = 1 + (K - 2) * (2 * CPW + 1);
+    constexpr int WAITLA = 1 + (K - 3) * (2 * CPW + 1);
+    constexpr int JLO = (OFFX + 1) / 2;
+    constexpr int EB = 16;                      // rows of parked border-column sums per flush
+    constexpr int PITCH = 2048;                 // ring row: 128 virtual lanes x 16 B
+    constexpr int SLOT = 2 * PITCH;
+    constexpr int OOB = 0x7ff00000;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t *const ring = lds;
+    int4 *const edgeSum = reinterpret_cast<int4 *>(lds + K * SLOT);  // [F][side][EB]
+    const uint32_t sinkLds = static_cast<uint32_t>(K * SLOT + 2 * CPW * 2 * EB * 16);
+
+    const LanczosDev &L = a.l;
+    const int lane = static_cast<int>(threadIdx.x) & 63;
+    const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    const int band = static_cast<int>(blockIdx.x);
+    const int y0 = a.rowBegin + band * a.rowsPerBand;
+    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;  // whole workgroup
+    const int np = a.np, fpw = a.fpw;
+    const int f0 = static_cast<int>(blockIdx.y) * fpw;
+    const int nF = min(fpw, a.frames - f0);     // frames of this workgroup
+    const int v = 62 * wib + lane;               // virtual lane
+    const int F = v >= 1 ? (v - 1) / (np + 1) : -1, k = v >= 1 ? (v - 1) - F * (np + 1) : -1;
+    const bool mine = F >= 0 && F < nF && k < np;  // holds frame F's columns [16k, 16k + 16)
+    const bool produce = mine && lane >= 1 && lane <= 62;
+    const int Fc = mine ? F : 0;
+    const int outX = 8 * k;
+    const bool laneL = produce && k == 0, laneR = produce && k == np - 1;
+
+    const int64_t sFrameSt = static_cast<int64_t>(a.io.srcFrameSt), dFrameSt = static_cast<int64_t>(a.io.dstFrameSt);
+    const uint8_t *srcBase = a.io.src + static_cast<int64_t>(f0) * sFrameSt;
+    uint8_t *dstBase = a.io.dst + static_cast<int64_t>(f0) * dFrameSt;
+    // this lane's frame (prologue loads, stores); the DMAs address each frame separately
+    const __amdgpu_buffer_rsrc_t srcL =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcBase + Fc * sFrameSt), 0, a.srcBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0;
+    const int voff = mine ? 16 * k : OOB;
+    const uint32_t ldsLane = static_cast<uint32_t>(16 * v);
+    const int dir = (band & 1) ? -1 : 1;
+    const int rFirst = 2 * y0 + L.offY;
+    const int rLast = 2 * (y1 - 1) + L.offY + NY - 1;
+    const int nRows = y1 - y0;
+    const uint32_t bias = opaque(1u << 19);
+    uint32_t cvx[NX / 2];
+#pragma unroll
+    for (int p = 0; p < NX / 2; ++p)
+        cvx[p] = opaque(L.cxo[p]);
+
+    const uint32_t ldsBase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint8_t *)lds));
+    const uint8_t *ringLane = ring + ldsLane;
+    auto row_soff = [&](int r) { return (r >= rFirst && r <= rLast) ? (r - srcRow0) * srcSt : OOB; };
+    auto rowAt = [&](int i, int t) { return dir > 0 ? rFirst + 2 * i + t : rLast - 2 * i - t; };
+    const int dmaSoff0 = (rowAt(0, NY - 2) - srcRow0) * srcSt, dmaStep = 2 * dir * srcSt, dmaNext = dir * srcSt;
+    const uint64_t rowMask = np >= 64 ? ~0ull : (1ull << np) - 1ull;  // the lanes of one frame row
+    // DMA of iteration j: frame slot c = wib + 2 jj (its rows at virtual lanes 1 + (np + 1) c ...);
+    // slots past the workgroup's frames DMA into the sink so every wave's vm count is the same
+    auto dma_iter = [&](int j, int slot) {
+        const uint32_t s = ldsBase + static_cast<uint32_t>(slot * SLOT);
+        const bool in = j < nRows;
+        const int so0 = in ? dmaSoff0 + j * dmaStep : OOB;
+        const int so1 = in ? dmaSoff0 + j * dmaStep + dmaNext : OOB;
+#pragma unroll
+        for (int jj = 0; jj < CPW; ++jj) {
+            const int c = wib + 2 * jj;
+            const bool real = c < nF;  // uniform
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t *>(srcBase + (real ? c : 0) * sFrameSt), 0, a.srcBytes, 0x00020000);
+            const int vv = real ? 16 * lane : OOB;
+            const uint32_t d0 = real ? s + static_cast<uint32_t>(16 * (1 + (np + 1) * c)) : ldsBase + sinkLds;
+            const uint32_t d1 = real ? d0 + PITCH : d0;
+            dma_row_masked(d0, vv, rs, so0, rowMask);
+            dma_row_masked(d1, vv, rs, so1, rowMask);
+        }
+    };
+    auto read_iter = [&](int slot, uint4 &r0, uint4 &r1) {
+        const uint8_t *p = ringLane + slot * SLOT;
+        r0 = *reinterpret_cast<const uint4 *>(p);
+        r1 = *reinterpret_cast<const uint4 *>(p + PITCH);
+    };
+    auto unpack_odd = [&](uint4 w, uint32_t (&q)[8]) {
+        const uint32_t r = static_cast<uint32_t>(
+            __builtin_amdgcn_mov_dpp(static_cast<int>(w.x), 0x130 /* wave_shl:1 */, 0xf, 0xf, true));
+        q[0] = __builtin_amdgcn_perm(0u, w.x, 0x0c020c01u);
+        q[1] = __builtin_amdgcn_perm(w.y, w.x, 0x0c040c03u);
+        q[2] = __builtin_amdgcn_perm(0u, w.y, 0x0c020c01u);
+        q[3] = __builtin_amdgcn_perm(w.z, w.y, 0x0c040c03u);
+        q[4] = __builtin_amdgcn_perm(0u, w.z, 0x0c020c01u);
+        q[5] = __builtin_amdgcn_perm(w.w, w.z, 0x0c040c03u);
+        q[6] = __builtin_amdgcn_perm(0u, w.w, 0x0c020c01u);
+        q[7] = __builtin_amdgcn_perm(r, w.w, 0x0c040c03u);
+    };
+    // border columns of rows [yb, yb + n) of the frames whose edge lanes this wave holds: lane i
+    // rewrites row yb + dir i of one (frame, side) per pass
+    const int vLo = 62 * wib + 1, vHi = 62 * wib + 62;  // this wave's producing virtual lanes
+    auto flush_edges = [&](int yb, int n) {
+        auto fix = [&](int sv, int kk) {
+            const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.xM[kk]) >> L.xT[kk];
+            return min(qq, 255u);
+        };
+        const int rowOff = (yb + dir * lane - a.io.dstRow0) * dstSt;
+        for (int G = 0; G < nF; ++G) {
+            const int vL = 1 + (np + 1) * G, vR = vL + np - 1;
+            uint8_t *dstF = dstBase + G * dFrameSt;
+            const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(dstF, 0, a.dstBytes, 0x00020000);
+            if (vL >= vLo && vL <= vHi) {
+                const int4 e = edgeSum[(G * 2 + 0) * EB + (lane & (EB - 1))];
+                const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
+                __builtin_amdgcn_raw_buffer_store_b32(w, dr, lane < n ? rowOff : OOB, 0, 0);
+            }
+            if (vR >= vLo && vR <= vHi) {
+                const int4 e = edgeSum[(G * 2 + 1) * EB + (lane & (EB - 1))];
+                const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
+                __builtin_amdgcn_raw_buffer_store_b32(w, dr, lane < n ? rowOff + L.dstW - 4 : OOB, 0, 0);
+            }
+        }
+    };
+
+    uint32_t win[NY][8];
+    {
+        uint4 w0[NY - 2];
+#pragma unroll
+        for (int t = 0; t < NY - 2; ++t) {
+            u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(srcL, voff, row_soff(rowAt(0, t)), 0);
+            w0[t] = make_uint4(q.x, q.y, q.z, q.w);
+        }
+#pragma unroll
+        for (int t = 0; t < NY - 2; ++t)
+            unpack_odd(w0[t], win[t]);
+    }
+    // zero every ring byte the DMAs never write (frame gaps, both ends) once
+    for (int i = static_cast<int>(threadIdx.x); i < K * 2 * 128; i += static_cast<int>(blockDim.x)) {
+        const int vv = i & 127;
+        const int FF = vv >= 1 ? (vv - 1) / (np + 1) : -1, kk = vv >= 1 ? (vv - 1) - FF * (np + 1) : -1;
+        if (!(FF >= 0 && FF < nF && kk < np))
+            *reinterpret_cast<uint4 *>(ring + (i >> 7) * PITCH + 16 * vv) = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const __amdgpu_buffer_rsrc_t dstL =
+        __builtin_amdgcn_make_buffer_rsrc(dstBase + Fc * dFrameSt, 0, a.dstBytes, 0x00020000);
+    const int stoff = produce ? outX : OOB;
+#pragma unroll
+    for (int j = 0; j < K - 1; ++j) {
+        dma_iter(j, j);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{0u, 0u}, dstL, OOB, 0, 0);  // dropped: steady-state vm order
+    }
+    uint4 n0, n1;
+    wait_vmcnt<WAIT>();
+    // the zeroed gaps (LDS writes) and every wave's DMA(0) are visible after the barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    read_iter(0, n0, n1);
+    auto row = [&](auto uc, int base) {
+        constexpr int vv = decltype(uc)::value;
+        const int i = base + vv;
+        if (i >= nRows)
+            return;
+        const int yy = dir > 0 ? y0 + i : y1 - 1 - i;
+        wait_vmcnt<WAITLA>();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        uint4 m0, m1;
+        read_iter((vv + 1) % K, m0, m1);
+        dma_iter(i + K - 1, (vv + K - 1) % K);
+        unpack_odd(n0, win[(2 * vv + NY - 2) % NY]);
+        unpack_odd(n1, win[(2 * vv + NY - 1) % NY]);
+        n0 = m0;
+        n1 = m1;
+        uint32_t acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const uint32_t p0 = win[(2 * vv) % NY][c] + win[(2 * vv + NY - 1) % NY][c];
+            acc[c] = C0ONE ? p0 : pk_mul(p0, L.cy[0]);
+        }
+#pragma unroll
+        for (int p = 1; p < H; ++p)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t pp = win[(2 * vv + p) % NY][c] + win[(2 * vv + NY - 1 - p) % NY][c];
+                acc[c] = pk_mad(pp, L.cy[p], acc[c]);
+            }
+        if (yy < L.mainBeginY || yy >= L.mainEndY) {
+            const bool top = yy < L.mainBeginY;
+            const int bi = top ? yy : yy - L.mainEndY;
+            const uint32_t m = top ? L.yTopM[bi] : L.yBotM[bi];
+            const int sh = top ? L.yTopS[bi] : L.yBotS[bi];
+#pragma unroll
+            for (int c = 0; c < 8; ++c)
+                acc[c] = ydiv2(acc[c], m, sh);
+        }
+        int sum[8];
+        asm volatile("s_nop 1" ::: "memory");
+#pragma unroll
+        for (int kx = 0; kx < 8; ++kx) {
+            int pFirst = -1;
+#pragma unroll
+            for (int p = 0; p < NX / 2; ++p) {
+                const int j = kx + p + JLO;
+                if (pFirst < 0 && j >= 1 && j <= 8)
+                    pFirst = p;
+            }
+            int sacc;
+            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[pFirst]), "v"(acc[kx + pFirst + JLO - 1]),
+                "v"(bias));
+#pragma unroll
+            for (int p = 0; p < NX / 2; ++p) {
+                const int j = kx + p + JLO;
+                if (p == pFirst)
+                    continue;
+                if (j <= 0)
+                    asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shr:1 row_mask:0xf bank_mask:0xf"
+                        : "+v"(sacc) : "v"(acc[j + 7]), "v"(cvx[p]));
+                else if (j >= 9)
+                    asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf"
+                        : "+v"(sacc) : "v"(acc[j - 9]), "v"(cvx[p]));
+                else
+                    sacc = sdot2(acc[j - 1], L.cxo[p], sacc);
+            }
+            sum[kx] = sacc;
+        }
+        u32x2 o;
+        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
+        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstL, stoff, (yy - a.io.dstRow0) * dstSt, 0);
+        // border columns: park the edge lanes' raw sums, flush every EB rows (every wave holds an
+        // edge lane of some frame, so the branch is per frame inside flush_edges)
+        const int slot = i & (EB - 1);
+        if (laneL)
+            edgeSum[(F * 2 + 0) * EB + slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+        if (laneR)
+            edgeSum[(F * 2 + 1) * EB + slot] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+        if (slot == EB - 1 || i == nRows - 1) {
+            __builtin_amdgcn_wave_barrier();
+            flush_edges(yy - dir * slot, slot + 1);
+        }
+    };
+    for (int base = 0; base < nRows; base += H)
+        static_for<H>([&](auto uc) { row(uc, base); });
+
+    wait_vmcnt<0>();
+}
 
 // ================================================================ general-ratio wave walker
 //
@@ -4063,6 +4328,15 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int lastLanes = (rowNeed - 16 - 1024 * (chunks - 1)) / 16;
     const int cpw = (chunks + wpr - 1) / wpr;
     const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
+    // narrow frames: several frames side by side in one 2-wave workgroup (lanczos_stack_kernel)
+    const int npf = l.srcW / 16;
+    const int fpwMax = npf >= 1 ? std::min(6, 125 / (npf + 1)) : 0;
+    // (only where a frame leaves most of a wave idle: 320 -> 160 columns, 5 frames per workgroup,
+    // 0.427 vs 0.529 ms per 16384 frames; at 3 frames of 640 columns (C1) it is no faster, and 3.5 %
+    // slower for Lanczos-3 640x360 -> 320x180, profiles/r03/stack_narrow.txt; option "stack" = 2
+    // forces it from 2 frames per workgroup)
+    const bool stack = shared && l.stack && wpr == 1 && l.srcW == 2 * l.dstW && l.srcW % 16 == 0 && np == npf &&
+                       fpwMax >= (l.stack >= 2 ? 2 : 4) && io.frames >= 2;
     // block-shared ring depth: prefetch 1-2 -> 3, 3 (default) -> the window period NY/2 (4 for
     // Lanczos-2, 5 for Lanczos-3: every ring slot index is then a compile-time constant; C2 x256
     // 0.5226 vs 0.532 ms at depth 4), 4 -> 5.  Depth 5 packs the ring rows to the bytes they need
@@ -4070,7 +4344,25 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int K = pd <= 2 ? 3 : pd == 3 ? (l.NY == 10 ? 5 : 4) : 5;
     const bool pack = l.ringPack || (shared && K == 5);
     const int rowPitch = pack ? rowNeed : 16 + 1024 * chunks;
-    if (shared) {
+    int fpw = 1;
+    if (stack) {
+        const bool one = (l.cy[0] & 0xffffu) == 1u;
+        fpw = std::min(fpwMax, io.frames);
+        const int scpw = (fpw + 1) / 2;
+        ldsBytes = l.NY / 2 * 4096 + scpw * 2 * 2 * IQO_SYMB_EDGE_BATCH * 16 + 1024;
+        block = 128;
+#define IQO_STACK_C(NY_, NX_, OX_, ONE_)                                                                \
+    (scpw == 1 ? reinterpret_cast<const void *>(lanczos_stack_kernel<NY_, NX_, OX_, NY_ / 2, 1, ONE_>)         \
+     : scpw == 2 ? reinterpret_cast<const void *>(lanczos_stack_kernel<NY_, NX_, OX_, NY_ / 2, 2, ONE_>)       \
+                 : reinterpret_cast<const void *>(lanczos_stack_kernel<NY_, NX_, OX_, NY_ / 2, 3, ONE_>))
+        if (l.NY == 10 && one)
+            kern = IQO_STACK_C(10, 12, -5, true);
+        else if (l.NY == 10)
+            kern = IQO_STACK_C(10, 12, -5, false);
+        else
+            kern = IQO_STACK_C(8, 8, -3, false);
+#undef IQO_STACK_C
+    } else if (shared) {
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         ldsBytes = K * 2 * rowPitch + 2 * IQO_SYMB_EDGE_BATCH * 16 + (cpw * wpr > chunks ? 1024 : 0);
@@ -4112,9 +4404,13 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
                : pd == 2 ? reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 2>)
                          : reinterpret_cast<const void *>(lanczos_stream_kernel<2, 2, 8, 10, -2, 3>);
     }
+    const int groups = stack ? (io.frames + fpw - 1) / fpw : io.frames;  // workgroup columns of the grid
     if (bands <= 0) {
         const int resident = resident_waves(kern, block, ldsBytes);
-        if (shared && l.rounds >= 0) {
+        if (stack) {
+            const int64_t want = static_cast<int64_t>(l.rounds > 0 ? l.rounds : 6) * (resident / 2);
+            bands = static_cast<int>(std::min<int64_t>((want + groups - 1) / groups, std::max(1, rows / 16)));
+        } else if (shared && l.rounds >= 0) {
             // block-shared ring: about `rounds` rounds of resident workgroups (default 6), bands of
             // >= 16 rows.  On fresh data more, shorter bands beat the one-round makespan optimum
             // (C2 x128: 8 bands 0.305 ms, 24 0.296, 48 0.294): workgroups that start and finish at
@@ -4131,7 +4427,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
     a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd,
-                    pack ? lastLanes : 64};
+                    pack ? lastLanes : 64, fpw, io.frames};
     // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -4142,12 +4438,12 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     a.srcBytes = static_cast<int>(sb);
     a.dstBytes = static_cast<int>(db);
     const int waves = bands * wpr;
-    P->grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(io.frames))
+    P->grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(groups))
                        : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
     P->block = block;
     P->lds = ldsBytes;
     P->kern = kern;
-    P->kind = shared ? 1 : (l.sym ? 2 : 0);
+    P->kind = stack ? 3 : shared ? 1 : (l.sym ? 2 : 0);
     P->pd = pd;
     return hipSuccess;
 }
@@ -4284,6 +4580,7 @@ hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const Lanc
     Prep<LanczosArgs> py, pu, pv;
     hipError_t e;
     LanczosDev lyGrid = ly;
+    lyGrid.stack = 0;  // the fused launch has one (band, frame) grid for all three planes
     if ((e = prep_lanczos(lyGrid, ioY, 0, ly.dstH, 0, &py)) != hipSuccess ||
         (e = prep_lanczos(lc, ioU, 0, lc.dstH, 0, &pu)) != hipSuccess ||
         (e = prep_lanczos(lc, ioV, 0, lc.dstH, 0, &pv)) != hipSuccess)

@@ -1191,3 +1191,57 @@ def test_ryx_matches_oracle(cfg):
     r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 1, dh * (dw + 1), dst.data_ptr())
     torch.cuda.synchronize()
     assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+
+
+STACK_SHAPES = [
+    (2, 640, 480, 320, 240, 7),   # C1: 3 frames per 2-wave workgroup, a partial last group
+    (3, 640, 360, 320, 180, 5),   # Lanczos-3 (window period 5)
+    (2, 320, 240, 160, 120, 11),  # 5 frames per workgroup
+    (3, 1024, 64, 512, 32, 4),    # 64 source lanes: 1 frame would fill a wave; 2 per workgroup
+    (2, 208, 30, 104, 15, 13),    # odd output height, 13 lanes per frame (6 frames, border rows)
+]
+
+
+@pytest.mark.parametrize("shape", STACK_SHAPES, ids=lambda s: "L%d_%dx%d_x%d" % (s[0], s[1], s[2], s[5]))
+def test_frame_stacked_streamer_matches_oracle(shape):
+    """Narrow frames side by side in one workgroup (lanczos_stack_kernel): every frame of a batch
+    whose size is not a multiple of the frames per workgroup, noise / flat / half-flat frames, band
+    splits; and the same batch through the one-frame-per-workgroup streamer (option stack = 0)."""
+    d, sw, sh, dw, dh, n = shape
+    frames = _noise_batch(n, sw, sh, 900)
+    frames[1] = 255
+    frames[2, :, : sw // 2] = 0
+    src = torch.from_numpy(frames).to(DEV)
+    exp = [ol.run_oracle("lanczos", d, sw, sh, dw, dh, 1, frames[f]) for f in range(n)]
+    ref = None
+    for stack, bands in ((2, 0), (2, 1), (2, 3), (1, 0), (0, 0)):
+        r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
+        r.set_option("stack", stack)
+        r.set_option("bands", bands)
+        out = r.resize_tensor(src).cpu().numpy()
+        for f in range(n):
+            bad = np.argwhere(out[f] != exp[f])
+            assert bad.size == 0, (shape, stack, bands, f, bad[:4].tolist())
+        if ref is None:
+            ref = out
+        assert (out == ref).all()
+
+
+def test_frame_stacked_c1_full_batch():
+    """C1's bench batch size through the stacked streamer equals the one-frame-per-workgroup
+    streamer on all 4096 frames, and frames 0, 2047, 4095 equal the oracle."""
+    sw, sh, dw, dh = 640, 480, 320, 240
+    g = torch.Generator(device=DEV)
+    g.manual_seed(4096)
+    src = torch.randint(0, 256, (4096, sh, sw), dtype=torch.uint8, device=DEV, generator=g)
+    r2 = libiqo_amd.LanczosResizer(2, sw, sh, dw, dh)
+    r2.set_option("stack", 2)
+    a = r2.resize_tensor(src)
+    r0 = libiqo_amd.LanczosResizer(2, sw, sh, dw, dh)
+    r0.set_option("stack", 0)
+    b = r0.resize_tensor(src)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    for f in (0, 2047, 4095):
+        exp = ol.run_oracle("lanczos", 2, sw, sh, dw, dh, 1, src[f].cpu().numpy())
+        assert (a[f].cpu().numpy() == exp).all(), f
