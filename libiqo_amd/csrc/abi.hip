@@ -247,10 +247,22 @@ void copy_rows(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, siz
 
 bool is_gfx950(int dev)
 {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+    // the device's architecture cannot change in a process: queried once per device (the
+    // property query costs more than building a small plan's tables)
+    static std::mutex mu;
+    static std::vector<signed char> known;  // -1 unknown, 0 / 1
+    std::lock_guard<std::mutex> g(mu);
+    if (dev < 0)
         return false;
-    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    if (static_cast<size_t>(dev) >= known.size())
+        known.resize(static_cast<size_t>(dev) + 1, -1);
+    if (known[static_cast<size_t>(dev)] < 0) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess)
+            return false;
+        known[static_cast<size_t>(dev)] = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+    }
+    return known[static_cast<size_t>(dev)] == 1;
 }
 
 template <typename T>
@@ -1211,7 +1223,33 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
         return IQO_HIP_ENOMEM;
 
     const int dstH = p.dstH;
-    const int bands = sBytes < kHostPipeMinBytes ? 1 : std::max(1, std::min(kHostBands, dstH / kHostBandRows));
+    if (sBytes < kHostPipeMinBytes) {
+        // small frame: upload, kernel and download in order on one stream, one synchronisation
+        // (the pipeline's events and cross-stream waits cost more than they overlap here)
+        const uint8_t *from = src;
+        size_t fromSt = srcSt;
+        if (!pinSrc) {
+            copy_rows(st->hSrc, sPitch, src, srcSt, W, static_cast<size_t>(p.srcH));
+            from = st->hSrc;
+            fromSt = sPitch;
+        }
+        if (hipMemcpy2DAsync(st->dSrc, sPitch, from, fromSt, W, static_cast<size_t>(p.srcH), hipMemcpyHostToDevice,
+                             st->sK) != hipSuccess)
+            return IQO_HIP_EHIP;
+        int rc = run_band(h, 1, 0, static_cast<size_t>(dstH), 0, sPitch, sBytes, st->dSrc, dPitch, dBytes, st->dDst,
+                          st->sK);
+        if (rc)
+            return rc;
+        uint8_t *to = pinDst ? dst : st->hDst;
+        if (hipMemcpy2DAsync(to, pinDst ? dstSt : dPitch, st->dDst, dPitch, w, static_cast<size_t>(dstH),
+                             hipMemcpyDeviceToHost, st->sK) != hipSuccess ||
+            hipStreamSynchronize(st->sK) != hipSuccess)
+            return IQO_HIP_EHIP;
+        if (!pinDst)
+            copy_rows(dst, dstSt, st->hDst, dPitch, w, static_cast<size_t>(dstH));
+        return IQO_HIP_OK;
+    }
+    const int bands = std::max(1, std::min(kHostBands, dstH / kHostBandRows));
     auto bandRow = [&](int b) { return static_cast<int>(static_cast<int64_t>(dstH) * b / bands); };
     int rowsUp = 0;  // source rows [0, rowsUp) are queued for upload
     for (int b = 0; b < bands; ++b) {
@@ -1410,8 +1448,57 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
                           const uint8_t *srcU, const uint8_t *srcV, size_t dstStY, uint8_t *dstY, size_t dstStUV,
                           uint8_t *dstU, uint8_t *dstV)
 {
-    if (!yp)
+    if (!yp || !yp->y || !yp->c || !srcY || !srcU || !srcV || !dstY || !dstU || !dstV)
         return IQO_HIP_EINVAL;
+    {
+        // small frames: the three planes staged into one buffer, one upload, the fused device
+        // launch (iqo_hip_resize_yuv420_device), one download, one synchronisation
+        const Plan &py = yp->y->p, &pc = yp->c->p;
+        const size_t W = static_cast<size_t>(py.srcW), H = static_cast<size_t>(py.srcH);
+        const size_t Wc = static_cast<size_t>(pc.srcW), Hc = static_cast<size_t>(pc.srcH);
+        const size_t w = static_cast<size_t>(py.dstW), hh = static_cast<size_t>(py.dstH);
+        const size_t wc = static_cast<size_t>(pc.dstW), hc = static_cast<size_t>(pc.dstH);
+        if (srcStY < W || srcStUV < Wc || dstStY < w || dstStUV < wc)
+            return IQO_HIP_EINVAL;
+        const size_t sY = (W + 15) & ~size_t(15), sC = (Wc + 15) & ~size_t(15);
+        const size_t dY = (w + 15) & ~size_t(15), dC = (wc + 15) & ~size_t(15);
+        const size_t oU = sY * H, oV = oU + sC * Hc, sBytes = oV + sC * Hc;
+        const size_t ou = dY * hh, ov = ou + dC * hc, dBytes = ov + dC * hc;
+        if (sBytes < kHostPipeMinBytes) {
+            DeviceGuard guard(yp->y->device);
+            if (!guard.ok())
+                return IQO_HIP_ENODEV;
+            HostStage *st = acquire_stage(yp->y->device);
+            if (!st)
+                return IQO_HIP_EHIP;
+            int rc = IQO_HIP_OK;
+            if (grow_device(&st->dSrc, &st->dSrcCap, sBytes) || grow_device(&st->dDst, &st->dDstCap, dBytes) ||
+                grow_pinned(&st->hSrc, &st->hSrcCap, sBytes) || grow_pinned(&st->hDst, &st->hDstCap, dBytes))
+                rc = IQO_HIP_ENOMEM;
+            if (!rc) {
+                copy_rows(st->hSrc, sY, srcY, srcStY, W, H);
+                copy_rows(st->hSrc + oU, sC, srcU, srcStUV, Wc, Hc);
+                copy_rows(st->hSrc + oV, sC, srcV, srcStUV, Wc, Hc);
+                if (hipMemcpyAsync(st->dSrc, st->hSrc, sBytes, hipMemcpyHostToDevice, st->sK) != hipSuccess)
+                    rc = IQO_HIP_EHIP;
+            }
+            if (!rc)
+                rc = iqo_hip_resize_yuv420_device(yp, 1, sY, sC, sBytes, st->dSrc, st->dSrc + oU, st->dSrc + oV, dY, dC,
+                                                  dBytes, st->dDst, st->dDst + ou, st->dDst + ov, st->sK, nullptr);
+            if (!rc && (hipMemcpyAsync(st->hDst, st->dDst, dBytes, hipMemcpyDeviceToHost, st->sK) != hipSuccess ||
+                        hipStreamSynchronize(st->sK) != hipSuccess))
+                rc = IQO_HIP_EHIP;
+            if (!rc) {
+                copy_rows(dstY, dstStY, st->hDst, dY, w, hh);
+                copy_rows(dstU, dstStUV, st->hDst + ou, dC, wc, hc);
+                copy_rows(dstV, dstStUV, st->hDst + ov, dC, wc, hc);
+            } else {
+                (void)hipStreamSynchronize(st->sK);
+            }
+            release_stage(st);
+            return rc;
+        }
+    }
     int rc = iqo_hip_resize(yp->y, srcStY, srcY, dstStY, dstY);
     if (!rc)
         rc = iqo_hip_resize(yp->c, srcStUV, srcU, dstStUV, dstU);
