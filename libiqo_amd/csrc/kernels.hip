@@ -1059,9 +1059,6 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 // row before it is refilled.  Waves with fewer chunks than CPW DMA into a sink so the vm-counter
 // pattern is the same in every wave.
 
-#ifndef IQO_SYMB_VORDER
-#define IQO_SYMB_VORDER 0  // vertical pass instruction order (A/B)
-#endif
 #ifndef IQO_SYMB_EXP
 #define IQO_SYMB_EXP 0  // timing experiments in variant builds (wrong output): 1 no vertical MACs,
                         // 2 half the horizontal dots, 3 / 4 dot2 / dot4 in place of the MACs
@@ -1310,27 +1307,6 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                 asm("v_dot4_i32_i8 %0, %1, %2, %0" : "+v"(acc[c]) : "s"(L.cy[p]), "v"(pp));
             }
 #else
-        {
-#if IQO_SYMB_VORDER == 1
-        // all pair sums of a tap pair first, then its 8 MACs (no add -> MAC back-to-back dependency)
-#pragma unroll
-        for (int p = 1; p < H; ++p) {
-            uint32_t pp[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                pp[c] = opaque(win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c]);
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                acc[c] = pk_mad(pp[c], L.cy[p], acc[c]);
-        }
-#elif IQO_SYMB_VORDER == 2
-        // packed 16-bit pair sums (v_pk_add_u16) feeding the MACs
-#pragma unroll
-        for (int p = 1; p < H; ++p)
-#pragma unroll
-            for (int c = 0; c < 8; ++c)
-                acc[c] = pk_mad(pk_add16(win[(2 * v + p) % NY][c], win[(2 * v + NY - 1 - p) % NY][c]), L.cy[p], acc[c]);
-#else
 #pragma unroll
         for (int p = 1; p < H; ++p)
 #pragma unroll
@@ -1338,8 +1314,6 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                 const uint32_t pp = win[(2 * v + p) % NY][c] + win[(2 * v + NY - 1 - p) % NY][c];
                 acc[c] = pk_mad(pp, L.cy[p], acc[c]);
             }
-#endif
-        }
 #endif
         if ((yy < L.mainBeginY || yy >= L.mainEndY) && !(dbg & 8)) {
             // border row (uniform, rare): rows outside the image were read as zero
