@@ -166,11 +166,13 @@ def cpu_baseline(cfg, seconds):
     return res
 
 
-def reference_benchmark_c1(cycles=256):
-    """C1 as the reference benchmark reports it (benchmark/benchmark.cpp:206-229, :1017-1033): an
-    I420 frame (Y 640x480, U and V 320x240; Lanczos-2, chroma pxScale 2), resizer objects
-    constructed inside the timed region, min ms over 256 cycles -- the reference's CPU path and
-    the drop-in HIP path (host pointers, same cycle) side by side."""
+def reference_benchmark(cfg, cycles=0):
+    """The workload as the reference benchmark reports it (benchmark/benchmark.cpp:206-229,
+    :1017-1033): one I420 frame (Y at the config's size, U and V at half size; Lanczos chroma
+    with pxScale 2), resizer objects constructed inside the timed region, min ms over the cycles
+    (256 as the reference for frames up to 1 Mpx, 16 above) -- the reference's CPU path (its own
+    TUs + CPUID dispatch, oracle/_ref) on 1 and on all usable host threads, beside the drop-in
+    HIP path through host pointers, same cycle."""
     import ctypes
 
     import numpy as np
@@ -180,30 +182,32 @@ def reference_benchmark_c1(cycles=256):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib as ol
 
-    W, H, w, h = 640, 480, 320, 240
+    m, d, W, H, w, h = cfg[:6]
+    cycles = cycles or (256 if W * H <= 1_000_000 else 16)
     rng = np.random.default_rng(0)
-    Y, U, V = (rng.integers(0, 256, s, dtype=np.uint8) for s in ((H, W), (H // 2, W // 2), (H // 2, W // 2)))
-    y, u, v = (np.zeros(s, np.uint8) for s in ((h, w), (h // 2, w // 2), (h // 2, w // 2)))
+    Y, U, V = (rng.integers(0, 256, sz, dtype=np.uint8) for sz in ((H, W), (H // 2, W // 2), (H // 2, W // 2)))
+    y, u, v = (np.zeros(sz, np.uint8) for sz in ((h, w), (h // 2, w // 2), (h // 2, w // 2)))
     u8p = ctypes.POINTER(ctypes.c_uint8)
     p = [a.ctypes.data_as(u8p) for a in (Y, U, V, y, u, v)]
-    out = {"cycles": cycles, "workload": "benchmark -m lanczos2 -iw 640 -ih 480 -ow 320 -oh 240 (I420, ctor in loop)"}
+    out = {"cycles": cycles, "workload": "benchmark -m %s -iw %d -ih %d -ow %d -oh %d (I420, ctor in loop)" %
+           ("%s%d" % (m, d) if m == "lanczos" else m, W, H, w, h)}
     _, _, usable = ol.host_cpus()
     if ol.ref_cpu_available():
         L = ol.ref_cpu()
         for nthr in sorted({1, usable}):
-            t = L.iqo_refcpu_bench_yuv420(0, 2, W, H, w, h, cycles, nthr, p[0], p[1], p[2], W, W // 2, p[3], p[4],
-                                          p[5], w, w // 2)
+            t = L.iqo_refcpu_bench_yuv420(ol.METHODS[m], d, W, H, w, h, cycles, nthr, p[0], p[1], p[2], W, W // 2,
+                                          p[3], p[4], p[5], w, w // 2)
             out["cpu_ms_per_cycle_%dthr" % nthr] = round(t * 1e3, 4)
         out["cpu_impl"] = L.iqo_refcpu_arch().decode()
     best = 1e9
     for _ in range(cycles):
         t0 = time.perf_counter()
-        r = libiqo_amd.Yuv420Resizer("lanczos", 2, W, H, w, h)
+        r = libiqo_amd.Yuv420Resizer(m, d, W, H, w, h)
         r.resize(W, Y, W // 2, U, V, w, y, w // 2, u, v)
         best = min(best, time.perf_counter() - t0)
         del r
     out["gpu_host_ptr_ms_per_cycle"] = round(best * 1e3, 4)
-    out["gpu_bit_exact_Y"] = bool((y == ol.run_oracle("lanczos", 2, W, H, w, h, 1, Y)).all())
+    out["gpu_bit_exact_Y"] = bool((y == ol.run_oracle(m, d, W, H, w, h, 1, Y)).all())
     return out
 
 
@@ -479,8 +483,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         log("cpu baseline: ~%.0f s" % args.cpu_seconds)
         cpu = cpu_baseline(cfg, args.cpu_seconds)
-        if args.config == "c1":
-            ref_bench = reference_benchmark_c1()
+        if args.config in ("c1", "c2", "c3", "c4"):
+            ref_bench = reference_benchmark(cfg)
 
     if rank == 0:
         value = out_px_step * args.steps / wall_max / 1e6

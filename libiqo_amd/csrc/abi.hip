@@ -12,8 +12,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -247,6 +249,93 @@ void copy_rows(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, siz
     }
     for (size_t r = 0; r < rows; ++r)
         std::memcpy(dst + r * dstSt, src + r * srcSt, w);
+}
+
+// Row copies between pageable user memory and the pinned staging of the host-pointer path, split
+// over a small process-wide thread pool: one thread's memcpy (~10 GB/s) is slower than the PCIe
+// link the staged rows then cross.  Created on first use and never torn down (as the staging
+// pool); one parallel copy at a time -- a caller that finds the pool busy copies alone.
+class CopyPool {
+public:
+    static CopyPool &instance()
+    {
+        static CopyPool *p = new CopyPool();
+        return *p;
+    }
+    void copy(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, size_t w, size_t rows)
+    {
+        std::unique_lock<std::mutex> use(useMu_, std::try_to_lock);
+        if (!use.owns_lock() || workers_.empty() || w * rows < (size_t(1) << 20) || rows < 32) {
+            copy_rows(dst, dstSt, src, srcSt, w, rows);
+            return;
+        }
+        std::unique_lock<std::mutex> g(mu_);
+        job_ = Job{dst, dstSt, src, srcSt, w, rows};
+        parts_ = static_cast<int>(workers_.size()) + 1;
+        next_ = 0;
+        remaining_ = parts_;
+        ++gen_;
+        cv_.notify_all();
+        while (next_ < parts_) {  // the caller takes parts too
+            const int part = next_++;
+            g.unlock();
+            run_part(part);
+            g.lock();
+            --remaining_;
+        }
+        done_.wait(g, [&] { return remaining_ == 0; });
+    }
+
+private:
+    struct Job {
+        uint8_t *dst;
+        size_t dstSt;
+        const uint8_t *src;
+        size_t srcSt, w, rows;
+    };
+    CopyPool()
+    {
+        const unsigned hw = std::thread::hardware_concurrency();
+        const unsigned n = hw >= 4 ? std::min(7u, hw / 2) : 0u;
+        for (unsigned i = 0; i < n; ++i)
+            workers_.emplace_back([this] { work(); });
+        for (auto &t : workers_)
+            t.detach();
+    }
+    void run_part(int part) const
+    {
+        const size_t r0 = job_.rows * static_cast<size_t>(part) / static_cast<size_t>(parts_);
+        const size_t r1 = job_.rows * static_cast<size_t>(part + 1) / static_cast<size_t>(parts_);
+        copy_rows(job_.dst + r0 * job_.dstSt, job_.dstSt, job_.src + r0 * job_.srcSt, job_.srcSt, job_.w, r1 - r0);
+    }
+    void work()
+    {
+        unsigned long seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return gen_ != seen; });
+            seen = gen_;
+            while (next_ < parts_) {
+                const int part = next_++;
+                g.unlock();
+                run_part(part);
+                g.lock();
+                if (--remaining_ == 0)
+                    done_.notify_all();
+            }
+        }
+    }
+    std::mutex useMu_, mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    Job job_{};
+    int parts_ = 0, next_ = 0, remaining_ = 0;
+    unsigned long gen_ = 0;
+};
+
+void copy_rows_par(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, size_t w, size_t rows)
+{
+    CopyPool::instance().copy(dst, dstSt, src, srcSt, w, rows);
 }
 
 bool is_gfx950(int dev)
@@ -1336,7 +1425,7 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
             size_t fromSt = srcSt;
             if (!pinSrc) {
                 uint8_t *pin = st->hSrc + static_cast<size_t>(rowsUp) * sPitch;
-                copy_rows(pin, sPitch, from, srcSt, W, n);
+                copy_rows_par(pin, sPitch, from, srcSt, W, n);
                 from = pin;
                 fromSt = sPitch;
             }
@@ -1366,7 +1455,7 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
             return IQO_HIP_EHIP;
         if (!pinDst) {
             const int r0 = bandRow(b), r1 = bandRow(b + 1);
-            copy_rows(dst + static_cast<size_t>(r0) * dstSt, dstSt, st->hDst + static_cast<size_t>(r0) * dPitch, dPitch,
+            copy_rows_par(dst + static_cast<size_t>(r0) * dstSt, dstSt, st->hDst + static_cast<size_t>(r0) * dPitch, dPitch,
                       w, static_cast<size_t>(r1 - r0));
         }
     }
