@@ -1245,3 +1245,25 @@ def test_frame_stacked_c1_full_batch():
     for f in (0, 2047, 4095):
         exp = ol.run_oracle("lanczos", 2, sw, sh, dw, dh, 1, src[f].cpu().numpy())
         assert (a[f].cpu().numpy() == exp).all(), f
+
+
+def test_plan_cache_resets_options():
+    """A destroyed plan is handed out again for an identical request (iqo_hip_plan_destroy keeps
+    it): the second plan must see default options, whatever the first one set."""
+    sw, sh, dw, dh = 960, 540, 640, 360  # the walker / d32 family: options change the kernel
+    frame = ol.gen("noise", sw, sh, 5)
+    exp = ol.run_oracle("lanczos", 3, sw, sh, dw, dh, 1, frame)
+    r = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh)
+    default_kernel = r.describe()["kernel"]
+    r.set_option("force_general", 1)
+    r.set_option("bands", 3)
+    assert r.describe()["kernel"] == "general"
+    del r
+    import gc
+    gc.collect()
+    for _ in range(3):
+        r2 = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh)
+        assert r2.describe()["kernel"] == default_kernel
+        assert (_run_host(r2, frame, dw, dh) == exp).all()
+        del r2
+        gc.collect()
