@@ -3006,9 +3006,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     const RyxDev &d = a.d;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int t = static_cast<int>(threadIdx.x);
-    const unsigned blk = xcd_spread(blockIdx.x, gridDim.x);
-    if (blk >= a.nBlocks)
+    const unsigned blk0 = xcd_spread(blockIdx.x, gridDim.x);
+    if (blk0 >= a.nBlocks)
         return;  // whole workgroup
+    // column part (d.parts workgroups per row), then band, then frame
+    const int part = static_cast<int>(blk0 % static_cast<unsigned>(d.parts));
+    const unsigned blk = blk0 / static_cast<unsigned>(d.parts);
+    const int cLo = d.parts > 1 ? d.cs[part] : 0, cHi = d.parts > 1 ? d.ce[part] : d.srcW;
+    const int xLo = d.parts > 1 ? d.xs[part] : 0, xHi = d.parts > 1 ? d.xs[part + 1] : d.dstW;
     const int band = static_cast<int>(blk % static_cast<unsigned>(a.bands));
     const int frame = static_cast<int>(blk / static_cast<unsigned>(a.bands));
     const int yb = a.groupBegin + band * a.rowsPerBand;  // a multiple of Q: first row of group mLo
@@ -3029,26 +3034,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #define IQO_RYX_EXP 0  // timing experiments (variant builds, wrong output): 1 no source loads, 2 no stores,
                        // 3 no barriers
 #endif
-    const int voff = 4 * t < d.srcW && IQO_RYX_EXP != 1 ? 4 * t : OOB;
+    const int span = cHi - cLo;  // this workgroup's source columns [cLo, cHi), 4 per thread
+    const int voff = 4 * t < span && IQO_RYX_EXP != 1 ? cLo + 4 * t : OOB;
 
-    // work rows: two buffers of (pad + srcW + pad) u16, zero padding written once
-    const int pitch = PADB + 2 * d.srcW + PADB;
-    for (int i = t; i < 2 * (PADB / 4); i += 512) {
+    // work rows: two buffers of (pad + span + pad) u16, zero padding written once
+    const int pitch = PADB + 2 * span + PADB;
+    for (int i = t; i < 2 * (PADB / 4); i += static_cast<int>(blockDim.x)) {
         const int buf = i / (PADB / 4), k = i % (PADB / 4);
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
-        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * d.srcW + 4 * k) = 0u;
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * span + 4 * k) = 0u;
     }
     // this thread's two output columns: table entries for the whole band
-    const int x0 = 2 * t;
+    const int x0 = xLo + 2 * t;
     uint32_t cf[2][NP];
     int aoff[2];
     uint32_t mm[2];
     int sh[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const int x = min(x0 + k, d.dstW - 1);
+        const int x = min(x0 + k, xHi - 1);
         const int4 c = d.cols[x];
-        aoff[k] = c.x;
+        aoff[k] = c.x - 2 * cLo;  // work-row byte offset relative to this part's first column
         mm[k] = static_cast<uint32_t>(c.y);
         sh[k] = c.z;
 #pragma unroll
@@ -3058,7 +3064,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     // interior Lanczos columns divide by 2^20 (magic_x: m = 2^31, shift 19), which is one
     // saturating pack of both columns; only the few border columns take the exact division
     const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
-    const int stoff = x0 < d.dstW && IQO_RYX_EXP != 2 ? x0 : OOB;  // dstW is even (launch_ryx)
+    const int stoff = x0 < xHi && IQO_RYX_EXP != 2 ? x0 : OOB;  // part bounds are even (launch_ryx)
 
     // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1.
     // Rows outside the image load as zero (the reference's masked border sums); rows past the
@@ -3127,7 +3133,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
             W[1] = ydiv2(W[1], d.yM[side][i], d.yS[side][i]);
         }
-        if (4 * t < d.srcW)
+        if (4 * t < span)
             *reinterpret_cast<uint2 *>(lds + B * pitch + PADB + 8 * t) = make_uint2(W[0], W[1]);
     };
 
@@ -4115,25 +4121,37 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     } else {
         return hipErrorInvalidValue;
     }
-    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * d.srcW);
+    int maxSpan = d.srcW;
+    if (d.parts == 2) {
+        if (d.xs[0] != 0 || d.xs[2] != d.dstW || d.xs[1] % 2 || d.cs[0] % 4 || d.cs[1] % 4 ||
+            d.ce[0] - d.cs[0] > 1024 || d.ce[1] - d.cs[1] > 1024 || d.xs[1] > 512 || d.dstW - d.xs[1] > 512)
+            return hipErrorInvalidValue;
+        maxSpan = std::max(d.ce[0] - d.cs[0], d.ce[1] - d.cs[1]);
+    } else if (d.parts != 1) {
+        return hipErrorInvalidValue;
+    }
+    const int threads = d.parts == 2 ? 256 : 512;
+    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
     const int groupBegin = rowBegin - rowBegin % d.Q;
     const int rows = rowEnd - groupBegin;
     // bands: ~2.5 rounds of resident workgroups, whole trips per band
     if (bands <= 0) {
-        const int64_t resident = std::max(1, resident_waves(kern, 512, ldsBytes) / 8);
-        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + io.frames - 1) / io.frames, std::max(1, rows / trip)));
+        const int64_t resident = std::max(1, resident_waves(kern, threads, ldsBytes) / (threads / 64));
+        const int64_t perBand = static_cast<int64_t>(io.frames) * d.parts;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / trip)));
     }
     bands = std::max(1, std::min(bands, (rows + d.Q - 1) / d.Q));
     int rpb = (rows + bands - 1) / bands;
     rpb = (rpb + d.Q - 1) / d.Q * d.Q;
     bands = (rows + rpb - 1) / rpb;
-    const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames);
+    const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames) * static_cast<uint64_t>(d.parts);
     if (nBlocks >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     RyxArgs a{d, io, rowBegin, rowEnd, groupBegin, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nBlocks)};
     void *args[] = {&a};
-    return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(512), args, static_cast<size_t>(ldsBytes), s);
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(static_cast<unsigned>(threads)), args,
+                           static_cast<size_t>(ldsBytes), s);
 }
 
 hipError_t launch_u23(const U23Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
