@@ -1063,12 +1063,6 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 #define IQO_SYMB_EXP 0  // timing experiments in variant builds (wrong output): 1 no vertical MACs,
                         // 2 half the horizontal dots, 3 / 4 dot2 / dot4 in place of the MACs
 #endif
-__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b)
-{
-    uint32_t r;
-    asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
 #ifndef IQO_SYMB_EDGE_BATCH
 #define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (C2: 64 -> 16 cuts write traffic +4.5% -> +2%)
 #endif
