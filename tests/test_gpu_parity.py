@@ -1228,6 +1228,25 @@ def test_frame_stacked_streamer_matches_oracle(shape):
         if ref is None:
             ref = out
         assert (out == ref).all()
+    # row bands through their source windows, and padded strides, on the stacked streamer
+    r = libiqo_amd.make_resizer("lanczos", d, sw, sh, dw, dh, 1)
+    r.set_option("stack", 2)
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = sorted({0, 1, dh // 3, dh // 2 + 1, dh - 2, dh})
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == ref).all(), (shape, "bands")
+    sst, dst_st = sw + 32, dw + 16
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 7, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == ref).all(), (shape, "padded")
+    assert (dbuf[:, :, dw:].cpu().numpy() == 7).all(), (shape, "wrote past the row")
 
 
 def test_frame_stacked_c1_full_batch():
