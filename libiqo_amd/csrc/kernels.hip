@@ -2983,8 +2983,11 @@ struct RyxArgs {
     unsigned nBlocks;
 };
 
+#ifndef IQO_RYX_WPE
+#define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
+#endif
 template <bool LZ, int P, int Q, int T, int OFF, int NP, int PD>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryx_kernel(RyxArgs a)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
 {
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
     constexpr int NW = (SPAN + P - 1) / P * P;    // register window rows (whole groups of P)
@@ -2996,7 +2999,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     static_assert(UQ % 2 == 0, "work-row buffer parity is static within a trip");
     // the next row's vertical pass overlaps this row's LDS reads when the read registers fit
     // beside the window (NP 10 would spill at 4 waves per SIMD)
-    constexpr bool PIPE = NP <= 8;
+    constexpr bool PIPE = NP <= 8 || NW <= 18;
     const RyxDev &d = a.d;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int t = static_cast<int>(threadIdx.x);
@@ -4101,13 +4104,14 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     // instantiations (plan.cpp build_ryx kShapes): method, P, Q, taps
     const void *kern = nullptr;
     int trip = 0;
-    if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 14 && (d.NP == 8 || d.NP == 10)) {
-        kern = d.NP == 8 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 14, -6, 8, 1>)
-                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 14, -6, 10, 1>);
-        trip = 4 * 3;
-    } else if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 10 && (d.NP == 6 || d.NP == 7)) {
-        kern = d.NP == 6 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 10, -4, 6, 1>)
-                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 10, -4, 7, 1>);
+    // (Lanczos: the reference's 14 / 10 taps less the two zero outer taps, plan.cpp build_ryx)
+    if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 12 && (d.NP == 8 || d.NP == 10)) {
+        kern = d.NP == 8 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 12, -5, 8, 1>)
+                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 12, -5, 10, 1>);
+        trip = 4 * 2;
+    } else if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 8 && (d.NP == 6 || d.NP == 7)) {
+        kern = d.NP == 6 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 8, -3, 6, 1>)
+                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 8, -3, 7, 1>);
         trip = 4 * 2;
     } else if (!d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 4 && d.NP == 3) {
         kern = reinterpret_cast<const void *>(ryx_kernel<false, 9, 4, 4, 0, 3, 1>);

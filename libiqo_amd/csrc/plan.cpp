@@ -1342,11 +1342,21 @@ void build_ryx(const Plan &p, RyxTables *t)
         if (ci.kind == kIdentity || ci.srcO != P * m + (P * j) / Q + off || ci.tabOff != j * T)
             return;
     }
-    t->rowCoef.resize(static_cast<size_t>(Q * T));
-    for (int k = 0; k < Q * T; ++k) {
-        const uint32_t c = static_cast<uint32_t>(p.y.table[static_cast<size_t>(k)]) & 0xffffu;
-        t->rowCoef[static_cast<size_t>(k)] = c * 0x10001u;
-    }
+    // Lanczos: the first and last taps of every phase quantise to zero at these ratios (the kernel
+    // windows start one row later and take two taps fewer: 4 of 28 row MACs at Lanczos-3, and a
+    // register window of 18 rows instead of 27); exact, since a zero tap adds nothing to the sum,
+    // and a masked border row's divisor is the reference's own (magic_y below)
+    const int trim = p.method == kLanczos ? 1 : 0;
+    for (int j = 0; j < Q && trim; ++j)
+        if (p.y.table[static_cast<size_t>(j * T)] != 0 || p.y.table[static_cast<size_t>(j * T + T - 1)] != 0)
+            return;
+    const int TE = T - 2 * trim;
+    t->rowCoef.resize(static_cast<size_t>(Q * TE));
+    for (int j = 0; j < Q; ++j)
+        for (int k = 0; k < TE; ++k) {
+            const uint32_t c = static_cast<uint32_t>(p.y.table[static_cast<size_t>(j * T + trim + k)]) & 0xffffu;
+            t->rowCoef[static_cast<size_t>(j * TE + k)] = c * 0x10001u;
+        }
     int m0 = 0, m1 = p.dstH;
     if (p.method == kLanczos) {
         m0 = -1;
@@ -1411,8 +1421,8 @@ void build_ryx(const Plan &p, RyxTables *t)
     }
     t->P = P;
     t->Q = Q;
-    t->taps = T;
-    t->off = off;
+    t->taps = TE;
+    t->off = off + trim;
     t->NP = NP;
     t->m0 = m0;
     t->m1 = m1;
