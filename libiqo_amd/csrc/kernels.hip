@@ -1450,7 +1450,8 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void l
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcBase + Fc * sFrameSt), 0, a.srcBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0;
-    const int voff = mine ? 16 * k : OOB;
+    const int dbg = IQO_DBG(a);  // variant builds: 1 no stores, 2 no source loads (timing only)
+    const int voff = mine && !(dbg & 2) ? 16 * k : OOB;
     const uint32_t ldsLane = static_cast<uint32_t>(16 * v);
     const int dir = (band & 1) ? -1 : 1;
     const int rFirst = 2 * y0 + L.offY;
@@ -1482,7 +1483,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void l
             const bool real = c < nF;  // uniform
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint8_t *>(srcBase + (real ? c : 0) * sFrameSt), 0, a.srcBytes, 0x00020000);
-            const int vv = real ? 16 * lane : OOB;
+            const int vv = real && !(dbg & 2) ? 16 * lane : OOB;
             const uint32_t d0 = real ? s + static_cast<uint32_t>(16 * (1 + (np + 1) * c)) : ldsBase + sinkLds;
             const uint32_t d1 = real ? d0 + PITCH : d0;
             dma_row_masked(d0, vv, rs, so0, rowMask);
@@ -1522,12 +1523,12 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void l
             if (vL >= vLo && vL <= vHi) {
                 const int4 e = edgeSum[(G * 2 + 0) * EB + (lane & (EB - 1))];
                 const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
-                __builtin_amdgcn_raw_buffer_store_b32(w, dr, lane < n ? rowOff : OOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(w, dr, lane < n && !(dbg & 1) ? rowOff : OOB, 0, 0);
             }
             if (vR >= vLo && vR <= vHi) {
                 const int4 e = edgeSum[(G * 2 + 1) * EB + (lane & (EB - 1))];
                 const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
-                __builtin_amdgcn_raw_buffer_store_b32(w, dr, lane < n ? rowOff + L.dstW - 4 : OOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(w, dr, lane < n && !(dbg & 1) ? rowOff + L.dstW - 4 : OOB, 0, 0);
             }
         }
     };
@@ -1553,7 +1554,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) void l
     }
     const __amdgpu_buffer_rsrc_t dstL =
         __builtin_amdgcn_make_buffer_rsrc(dstBase + Fc * dFrameSt, 0, a.dstBytes, 0x00020000);
-    const int stoff = produce ? outX : OOB;
+    const int stoff = produce && !(dbg & 1) ? outX : OOB;
 #pragma unroll
     for (int j = 0; j < K - 1; ++j) {
         dma_iter(j, j);
