@@ -60,6 +60,7 @@ struct iqo_hip_plan {
     int ryxSplit = 1;       // ratio-Y kernel: two 4-wave workgroups per row (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
+    int ratioAlt = 1;       // 3:2 kernel: odd row bands walk bottom-up (speed only)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
     // it off, leaving general_kernel)
@@ -564,6 +565,7 @@ void reset_options(iqo_hip_plan *h)
     h->ryxSplit = 1;
     h->lanes = 0;
     h->ratioPrefetch = 0;
+    h->ratioAlt = 1;
     h->chunkFrames = 0;
     h->useTile = h->useWalk = h->useUp2 = h->useD32 = h->useD31 = h->useRyx = h->useL23 = h->useU23 = h->useA32 = true;
 }
@@ -830,6 +832,7 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     d.dstH = h->p.dstH;
     d.np = h->lanes;
     d.pd = h->ratioPrefetch;
+    d.alt = h->ratioAlt;
     d.variant = t.variant;
     std::memcpy(d.cy, t.cy, sizeof d.cy);
     std::memcpy(d.cx, t.cx, sizeof d.cx);
@@ -1327,6 +1330,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "a32")) {  // 0: exact 3:2 Area downscales use the wave walker alone
         h->useA32 = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ratio_alt")) {  // 3:2 kernel: odd row bands walk bottom-up (speed only)
+        h->ratioAlt = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "ratio_prefetch")) {  // exact-ratio kernels: row groups loaded ahead (speed only);

@@ -2526,7 +2526,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
 {
     constexpr int NW = (GW + 2) / 3 * 3;  // register window rows (a multiple of the 3 rows a group adds)
     constexpr int U = NW / 3;             // groups per unrolled trip (window slots repeat)
-    static_assert(GW >= 3 && NTY <= 8 && NPX <= 5 && PO1 + NTY <= GW, "tap structure");
+    static_assert(GW >= 3 && NTY <= 8 && NPX <= 5 && PO1 + NTY == GW, "tap structure (mirror-symmetric)");
     static_assert(BX0 >= -4 && 9 + BX0 + 1 + 2 * NPX - 1 <= 15, "column windows within the lane's work pairs");
     constexpr int OOB = 0x7ff00000;
     static_assert(U % PD == 0, "prefetch slots repeat within a trip");
@@ -2547,6 +2547,14 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         return;
     const int kLo = yb >> 1;
     const int nG = (y1 - yb + 1) >> 1;  // groups of this band (dropped rows at either end)
+    // Odd bands walk bottom-up (d.alt): the halo rows two neighbouring bands share are then read
+    // by both at the same time (both at their ends, or both at their starts) and the second read
+    // hits L2 instead of HBM.  Walking up, relative row q is source row rLast - q and group g is
+    // group kLo + nG - 1 - g; group row x of the forward walk is window row GW - 1 - x, so with
+    // PO1 + NTY = GW the first output of a group (window rows 0 .. NTY-1) is the odd row with the
+    // odd phase's taps reversed and the second (rows PO1 ..) the even row with the even taps reversed.
+    const bool up = d.alt && (band & 1);
+    const int mTop = kLo + nG - 1;
 
     const int opw = 8 * a.np;
     const int x0 = max(0, min(wcol * opw, d.dstW - opw));
@@ -2573,9 +2581,9 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     const int rLast = 3 * (kLo + nG - 1) + GA + GW - 1;
     const int srcLast = a.io.srcRowEnd - 1;
     auto load_row = [&](int q) -> u32x3 {
-        const int r = rBase + q;
+        const int r = up ? rLast - q : rBase + q;
         const int rc = min(max(r, srcRow0), srcLast);
-        const bool in = r >= 0 && r < d.srcH && r <= rLast;
+        const bool in = r >= 0 && r < d.srcH && (up ? r >= rBase : r <= rLast);
         return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
     };
     auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
@@ -2627,7 +2635,8 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
             }
         }
     };
-    // once per trip: lane r < 2U rewrites the edge bytes of row yt + r from the parked sums
+    // once per trip: lane r < 2U rewrites the edge bytes of row yt + r (walking up: yt - r) from
+    // the parked sums
     auto flush = [&](int yt) {
         u32x2 oL = {0u, 0u}, oR = {0u, 0u};
         if (edgeL || edgeR) {  // uniform
@@ -2646,7 +2655,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
             if (edgeR)
                 oR = fix(1);
         }
-        const int y = yt + lane;
+        const int y = up ? yt - lane : yt + lane;
         const bool ok = lane < 2 * U && y >= y0 && y < y1;
         store_row(oL, edgeL ? 0 : OOB, y, ok);
         store_row(oR, edgeR ? d.dstW - 8 : OOB, y, ok);
@@ -2664,6 +2673,13 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         }
     };
 
+    // the two outputs' taps in walk order (uniform: SGPRs)
+    uint32_t cA[NTY], cB[NTY];
+#pragma unroll
+    for (int t = 0; t < NTY; ++t) {
+        cA[t] = up ? d.cy[1][NTY - 1 - t] : d.cy[0][t];
+        cB[t] = up ? d.cy[0][NTY - 1 - t] : d.cy[1][t];
+    }
     uint32_t R[NW][6];
     // the window of group 0 without the rows group 0 itself adds: relative rows 0 .. GW-4 -> slots
 #pragma unroll
@@ -2695,30 +2711,30 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
 #pragma unroll
             for (int i = 0; i < 3; ++i)
                 pre[v % PD][i] = load_row(3 * (g + PD) + GW - 3 + i);
-            const int y = 2 * (kLo + g);
+            const int yA = up ? 2 * (mTop - g) + 1 : 2 * (kLo + g), yB = up ? yA - 1 : yA + 1;
             uint32_t W[6];
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-                W[c] = pk_mul(R[(3 * v) % NW][c], d.cy[0][0]);
+                W[c] = pk_mul(R[(3 * v) % NW][c], cA[0]);
 #pragma unroll
             for (int t = 1; t < NTY; ++t)
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
-                    W[c] = pk_mad(R[(3 * v + t) % NW][c], d.cy[0][t], W[c]);
-            border_row(W, y);
-            emit(W, y, 2 * v);
+                    W[c] = pk_mad(R[(3 * v + t) % NW][c], cA[t], W[c]);
+            border_row(W, yA);
+            emit(W, yA, 2 * v);
 #pragma unroll
             for (int c = 0; c < 6; ++c)
-                W[c] = pk_mul(R[(3 * v + PO1) % NW][c], d.cy[1][0]);
+                W[c] = pk_mul(R[(3 * v + PO1) % NW][c], cB[0]);
 #pragma unroll
             for (int t = 1; t < NTY; ++t)
 #pragma unroll
                 for (int c = 0; c < 6; ++c)
-                    W[c] = pk_mad(R[(3 * v + PO1 + t) % NW][c], d.cy[1][t], W[c]);
-            border_row(W, y + 1);
-            emit(W, y + 1, 2 * v + 1);
+                    W[c] = pk_mad(R[(3 * v + PO1 + t) % NW][c], cB[t], W[c]);
+            border_row(W, yB);
+            emit(W, yB, 2 * v + 1);
         });
-        flush(2 * (kLo + base));
+        flush(up ? 2 * (mTop - base) + 1 : 2 * (kLo + base));
     }
 }
 

@@ -87,6 +87,7 @@ struct D32Dev {
     int np;                      // producing lanes per wave (0 = auto)
     int pd;                      // row groups loaded ahead (1, 2, 4; 0 = default 1)
     int variant;                 // tap structure: 0 Lanczos-3 (10 taps), 1 Lanczos-2 (6 taps)
+    int alt;                     // odd row bands walk bottom-up (speed only)
     uint32_t cy[2][8];           // (c, c) u16 splats: phase p's taps at group rows 2p .. 2p + 7
     uint32_t cx[2][5];           // phase p's (c_2q, c_2q+1) int16 pairs
     uint32_t xM[2][8];           // edge-lane exact divisions (left / right 8 columns)

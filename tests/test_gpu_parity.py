@@ -796,9 +796,10 @@ D32_SHAPES = [
 def test_lanczos_d32_matches_oracle(cfg):
     """Exact 3:2 Lanczos-3 downscale: lanczos_d32_kernel on every row and column (masked border
     rows and columns divided in the kernel); equal to the oracle on noise, flat and
-    half-flat frames; with option d32 = 0 (walker alone), in several band splits and lane counts,
-    in row bands through their source windows (odd band edges), with padded strides (d32 again)
-    and a destination stride that is not 8-byte aligned (walker alone)."""
+    half-flat frames; with option d32 = 0 (walker alone), in several band splits (odd bands walk
+    bottom-up; ratio_alt = 0: every band top-down) and lane counts, in row bands through their
+    source windows (odd band edges), with padded strides (d32 again) and a destination stride that
+    is not 8-byte aligned (walker alone)."""
     m, d, sw, sh, dw, dh, px = cfg
     n = 3
     frames = _noise_batch(n, sw, sh, 1700)
@@ -816,7 +817,8 @@ def test_lanczos_d32_matches_oracle(cfg):
     w.set_option("d32", 0)
     assert w.describe()["kernel"] in ("walk", "tile")
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
-    for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 8), ("lanes", 62)):
+    for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 8), ("lanes", 62),
+                     ("ratio_alt", 0)):
         b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
         b.set_option(opt, val)
         assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
