@@ -57,7 +57,7 @@ struct iqo_hip_plan {
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
-    int ryxSplit = 1;       // ratio-Y kernel: two 4-wave workgroups per row (speed only)
+    int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int ratioAlt = 1;       // 3:2 kernel: odd row bands walk bottom-up (speed only)
@@ -892,18 +892,21 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // Lanczos: two workgroups per row (4 waves each, half the columns) when each half's source
     // span fits 256 threads x 4 columns: barriers over 4 waves instead of 8 (1080p -> 480p:
     // Lanczos-2 0.171 vs 0.182 ms, Lanczos-3 0.232 vs 0.239; Area 5 % slower, so not for Area;
-    // profiles/r03/ryx_split.txt; option "ryx_split" = 0: off)
+    // profiles/r03/ryx_split.txt; option "ryx_split" = 0: off, 2: four 2-wave workgroups)
     d.parts = 1;
-    d.xs[0] = 0;
-    d.xs[1] = d.xs[2] = d.dstW;
-    d.cs[0] = d.cs[1] = 0;
-    d.ce[0] = d.ce[1] = d.srcW;
-    if (h->ryxSplit && d.lanczos && d.dstW >= 64) {
-        const int half = (d.dstW / 2 + 1) & ~1;  // even (2 outputs per thread)
-        const int xs[3] = {0, half, d.dstW};
-        int cs[2], ce[2];
+    for (int k = 0; k < 5; ++k)
+        d.xs[k] = k == 0 ? 0 : d.dstW;
+    for (int k = 0; k < 4; ++k) {
+        d.cs[k] = 0;
+        d.ce[k] = d.srcW;
+    }
+    const int P = h->ryxSplit >= 2 ? 4 : 2, threads = 512 / P;
+    if (h->ryxSplit && d.lanczos && d.dstW >= 32 * P) {
+        int xs[5], cs[4], ce[4];
+        for (int k = 0; k <= P; ++k)
+            xs[k] = k == 0 ? 0 : k == P ? d.dstW : (k * d.dstW / P + 1) & ~1;  // even (2 outputs per thread)
         bool ok = true;
-        for (int k = 0; k < 2 && ok; ++k) {
+        for (int k = 0; k < P && ok; ++k) {
             int lo = 1 << 30, hi = -(1 << 30);
             for (int x = xs[k]; x < xs[k + 1]; ++x) {
                 const int a = t.cols[static_cast<size_t>(x) * 4] / 2 - iqo_amd::kRyxPad;  // even window start
@@ -911,14 +914,15 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
                 hi = std::max(hi, a + 2 * t.NP);
             }
             cs[k] = k == 0 ? 0 : std::max(0, lo) & ~3;
-            ce[k] = k == 1 ? d.srcW : std::min(d.srcW, (hi + 3) & ~3);
-            ok = ce[k] - cs[k] <= 1024 && xs[k + 1] - xs[k] <= 512 && (k == 0 || lo >= 0) && (k == 1 || hi <= d.srcW);
+            ce[k] = k == P - 1 ? d.srcW : std::min(d.srcW, (hi + 3) & ~3);
+            ok = ce[k] - cs[k] <= 4 * threads && xs[k + 1] - xs[k] <= 2 * threads && (k == 0 || lo >= 0) &&
+                 (k == P - 1 || hi <= d.srcW);
         }
         if (ok) {
-            d.parts = 2;
-            std::copy(xs, xs + 3, d.xs);
-            std::copy(cs, cs + 2, d.cs);
-            std::copy(ce, ce + 2, d.ce);
+            d.parts = P;
+            std::copy(xs, xs + P + 1, d.xs);
+            std::copy(cs, cs + P, d.cs);
+            std::copy(ce, ce + P, d.ce);
         }
     }
     return d;
@@ -1257,8 +1261,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->rounds = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "ryx_split")) {  // ratio-Y kernel: two workgroups per row (speed only)
-        h->ryxSplit = value != 0;
+    if (!std::strcmp(key, "ryx_split")) {  // ratio-Y kernel: 0 / 1 / 2: one / two / four workgroups per row (speed only)
+        if (value < 0 || value > 2)
+            return IQO_HIP_EINVAL;
+        h->ryxSplit = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stack")) {  // narrow frames side by side in one workgroup (speed only):

@@ -4136,16 +4136,23 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     } else {
         return hipErrorInvalidValue;
     }
-    int maxSpan = d.srcW;
-    if (d.parts == 2) {
-        if (d.xs[0] != 0 || d.xs[2] != d.dstW || d.xs[1] % 2 || d.cs[0] % 4 || d.cs[1] % 4 ||
-            d.ce[0] - d.cs[0] > 1024 || d.ce[1] - d.cs[1] > 1024 || d.xs[1] > 512 || d.dstW - d.xs[1] > 512)
-            return hipErrorInvalidValue;
-        maxSpan = std::max(d.ce[0] - d.cs[0], d.ce[1] - d.cs[1]);
-    } else if (d.parts != 1) {
+    if (d.parts != 1 && d.parts != 2 && d.parts != 4)
         return hipErrorInvalidValue;
+    const int threads = 512 / d.parts;
+    int maxSpan = d.srcW;
+    if (d.parts > 1) {
+        // part k: output columns [xs[k], xs[k+1]) (even bounds, <= 2 per thread), source columns
+        // [cs[k], ce[k]) (multiples of 4, <= 4 per thread)
+        if (d.xs[0] != 0 || d.xs[d.parts] != d.dstW)
+            return hipErrorInvalidValue;
+        maxSpan = 0;
+        for (int k = 0; k < d.parts; ++k) {
+            if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > 2 * threads || d.cs[k] % 4 ||
+                d.cs[k] < 0 || d.ce[k] > d.srcW || d.ce[k] - d.cs[k] > 4 * threads || d.ce[k] <= d.cs[k])
+                return hipErrorInvalidValue;
+            maxSpan = std::max(maxSpan, d.ce[k] - d.cs[k]);
+        }
     }
-    const int threads = d.parts == 2 ? 256 : 512;
     const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
     const int groupBegin = rowBegin - rowBegin % d.Q;
     const int rows = rowEnd - groupBegin;

@@ -128,8 +128,8 @@ struct RyxDev {
     const uint32_t *colCoef;     // dstW x NP pairs
     // column split: `parts` workgroups per (band, frame), part k writes output columns
     // [xs[k], xs[k+1]) from source columns [cs[k], ce[k]) (multiples of 4); parts = 1: the whole row
-    int parts;
-    int xs[3], cs[2], ce[2];
+    int parts;                   // 1, 2 or 4
+    int xs[5], cs[4], ce[4];
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

@@ -1173,9 +1173,10 @@ def test_ryx_matches_oracle(cfg):
         b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
         b.set_option("bands", val)
         assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, val)
-    one = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)  # one 8-wave workgroup per row
-    one.set_option("ryx_split", 0)
-    assert (one.resize_tensor(src).cpu().numpy() == out).all(), cfg
+    for split in (0, 2):  # one 8-wave workgroup per row; four 2-wave workgroups per row
+        one = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+        one.set_option("ryx_split", split)
+        assert (one.resize_tensor(src).cpu().numpy() == out).all(), (cfg, split)
     got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
     cuts = [0, 3, dh // 3 + 1, dh // 2, dh - 5, dh]
     for r0, r1 in zip(cuts[:-1], cuts[1:]):
