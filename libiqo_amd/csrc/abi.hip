@@ -60,7 +60,7 @@ struct iqo_hip_plan {
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
-    int ratioAlt = 1;       // 3:2 kernel: odd row bands walk bottom-up (speed only)
+    int ratioAlt = 1;       // 3:2 and 3:1 kernels: odd row bands walk bottom-up (speed only)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
     // it off, leaving general_kernel)
@@ -855,6 +855,7 @@ iqo_amd::D31Dev d31_dev(const iqo_hip_plan *h)
     d.dstH = h->p.dstH;
     d.np = h->lanes;
     d.pd = h->ratioPrefetch;
+    d.alt = h->ratioAlt;
     d.variant = t.variant;
     d.cc = t.cc;
     std::memcpy(d.cp, t.cp, sizeof d.cp);
@@ -1338,7 +1339,7 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->useA32 = value != 0;
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "ratio_alt")) {  // 3:2 kernel: odd row bands walk bottom-up (speed only)
+    if (!std::strcmp(key, "ratio_alt")) {  // 3:2 / 3:1 kernels: odd row bands walk bottom-up (speed only)
         h->ratioAlt = value != 0;
         return IQO_HIP_OK;
     }

@@ -2800,6 +2800,7 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
     constexpr int OWN = -S::EB / 2;          // E index of the lane's own pair 0
     static_assert(U % PD == 0, "prefetch slots repeat within a trip");
     static_assert(OWN - S::NL >= 0 && OWN + 6 + S::NL == S::NE, "work pairs: NL from each neighbour");
+    static_assert(2 * S::CEN == S::NR - 1, "window symmetric about its centre row (bottom-up bands)");
     const D31Dev &d = a.d;
     __shared__ int4 park[4][2][8];  // per wave, side, row slot: the edge lane's 4 raw sums
     const int lane = static_cast<int>(threadIdx.x) & 63;
@@ -2816,6 +2817,9 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
     if (y0 >= y1)
         return;
     const int nR = y1 - y0;
+    // odd bands walk bottom-up (d.alt; as lanczos_d32_kernel): the window is symmetric about its
+    // centre row (2 CEN = NR - 1), so walking up is the same arithmetic on the rows in reverse
+    const bool up = d.alt && (band & 1);
 
     const int opw = 4 * a.np;
     const int x0 = max(0, min(wcol * opw, d.dstW - opw));
@@ -2841,9 +2845,9 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
     const int rLast = 3 * (y1 - 1) + S::YA + S::NR - 1;
     const int srcLast = a.io.srcRowEnd - 1;
     auto load_row = [&](int q) -> u32x3 {
-        const int r = rBase + q;
+        const int r = up ? rLast - q : rBase + q;
         const int rc = min(max(r, srcRow0), srcLast);
-        const bool in = r >= 0 && r < d.srcH && r <= rLast;
+        const bool in = r >= 0 && r < d.srcH && (up ? r >= rBase : r <= rLast);
         return __builtin_amdgcn_raw_buffer_load_b96(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
     };
     auto widen = [&](u32x3 v, uint32_t (&P)[6]) {
@@ -2891,7 +2895,8 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
                 park[wib][laneL ? 0 : 1][slot] = make_int4(sum[0], sum[1], sum[2], sum[3]);
         }
     };
-    // once per trip: lane r < U rewrites the 4 edge bytes of row yt + r from the parked sums
+    // once per trip: lane r < U rewrites the 4 edge bytes of row yt + r (walking up: yt - r) from
+    // the parked sums
     auto flush = [&](int yt) {
         uint32_t oL = 0u, oR = 0u;
         if (edgeL || edgeR) {  // uniform
@@ -2910,7 +2915,7 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
             if (edgeR)
                 oR = fix(1);
         }
-        const int y = yt + lane;
+        const int y = up ? yt - lane : yt + lane;
         const bool ok = lane < U && y >= y0 && y < y1;
         store_row(oL, edgeL ? 0 : OOB, y, ok);
         store_row(oR, edgeR ? d.dstW - 4 : OOB, y, ok);
@@ -2968,10 +2973,11 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
                 for (int c = 0; c < 6; ++c)
                     W[c] = pk_mad(R[(3 * v + S::CEN - S::DIST[k]) % NW][c] + R[(3 * v + S::CEN + S::DIST[k]) % NW][c],
                                   d.cp[k], W[c]);
-            border_row(W, y0 + g);
-            emit(W, y0 + g, v);
+            const int y = up ? y1 - 1 - g : y0 + g;
+            border_row(W, y);
+            emit(W, y, v);
         });
-        flush(y0 + base);
+        flush(up ? y1 - 1 - base : y0 + base);
     }
 }
 

@@ -104,6 +104,7 @@ struct D31Dev {
     int np;                      // producing lanes per wave (0 = auto)
     int pd;                      // output rows loaded ahead (Lanczos-3: 1, 5; Lanczos-2: 1, 2, 4; 0 = 1)
     int variant;                 // tap structure: 0 Lanczos-3 (18 taps), 1 Lanczos-2 (12 taps)
+    int alt;                     // odd row bands walk bottom-up (speed only)
     uint32_t cc, cp[5];          // (c, c) u16 splats: the centre tap, the symmetric pairs' taps
     uint32_t cxe[9], cxo[9];     // (c_2q, c_2q+1) / (c_2q+1, c_2q+2) int16 pairs: even / odd window starts
     uint32_t xM[2][4];           // edge-lane exact divisions (left / right 4 columns)

@@ -1102,7 +1102,8 @@ def test_lanczos_d31_matches_oracle(cfg):
     assert w.describe()["kernel"] in ("walk", "tile")
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
     pds = (1, 5) if d == 3 else (1, 2, 4)
-    for opt, val in [("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 8), ("lanes", 62)] + \
+    for opt, val in [("bands", 1), ("bands", 3), ("bands", 7), ("bands", dh), ("lanes", 8), ("lanes", 62),
+                     ("ratio_alt", 0)] + \
             [("ratio_prefetch", p) for p in pds]:
         b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
         b.set_option(opt, val)
