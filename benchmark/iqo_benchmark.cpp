@@ -9,6 +9,7 @@
 //   -cycles N    number of cycles (default 256, as the reference)
 //   -check FILE  write the Y-plane output to FILE (raw U8, stride = width) for parity checks
 //   -reuse 1     construct the resizers once, outside the timed region
+#include <iqo_hip.h>
 #include <libiqo/iqo.hpp>
 
 #include <algorithm>
@@ -170,5 +171,8 @@ int main(int argc, char **argv)
             std::fwrite(d.buf.data() + d.y() + y * d.st, 1, ow, f);
         std::fclose(f);
     }
+    int onHip = 0, onCpu = 0;
+    iqo_dropin_backend_counts(&onHip, &onCpu);
+    std::printf("  backend: hip %d cpu %d\n", onHip, onCpu);
     return 0;
 }

@@ -75,6 +75,7 @@ typedef struct {
     int phasesX, phasesY;   /* reference table counts (m_NumTablesX/Y) */
     int kernel;             /* IQO_KERNEL_* used for full frames with aligned layouts */
     int bandsPerFrame;      /* fast-path row bands per frame (tuning) */
+    int tileRows;           /* output rows per tile of IQO_KERNEL_TILE (option "tile_rows"; 0 = no tile tables) */
 } iqo_hip_plan_desc;
 
 /* Number of usable gfx950 devices (0 when none or the runtime is unusable). */
@@ -92,6 +93,14 @@ int iqo_hip_plan_linear(size_t srcW, size_t srcH, size_t dstW, size_t dstH, int 
 void iqo_hip_plan_destroy(iqo_hip_plan *plan);
 
 int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
+
+/* Upload the plan's device tables now (one allocation + one blocking copy on the plan's device)
+ * instead of inside the first resize call that needs them.  Call it before capturing resize calls
+ * into a hipGraph or issuing them on a stream that must not synchronise with the host: the lazy
+ * upload would otherwise do a hipMalloc and a blocking null-stream copy inside that first call
+ * (and report IQO_HIP_ENOMEM there).  Plans whose kernels take their coefficients as kernel
+ * arguments (the specialised fast kernels) have nothing to upload; the call is then a no-op. */
+int iqo_hip_plan_prepare(iqo_hip_plan *plan);
 
 /* Options (tests / tuning): "force_general" (0/1: every shape through IQO_KERNEL_GENERAL),
  * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
@@ -200,7 +209,9 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
                         size_t pxScale);
 
 /* Drop-in classes (iqo::LanczosResizer, AreaResizer, LinearResizer): how many objects this process constructed on the
- * HIP backend and on the CPU backend (no gfx950 device; IQO_REQUIRE_HIP=1 forbids it). */
+ * HIP backend, and on the CPU backend (no gfx950 device) plus the resize() calls of HIP objects that fell back to the
+ * CPU (a device failure, or a call the HIP path rejected).  IQO_REQUIRE_HIP=1 makes any CPU use abort;
+ * IQO_DROPIN_REPORT=1 prints the counts at exit (libiqo_amd/csrc/resizers.cpp). */
 void iqo_dropin_backend_counts(int *hip, int *cpu);
 
 #ifdef __cplusplus

@@ -35,7 +35,7 @@ class PlanDesc(ctypes.Structure):
     _fields_ = [("method", ctypes.c_int), ("device", ctypes.c_int), ("srcW", _c_sz), ("srcH", _c_sz),
                 ("dstW", _c_sz), ("dstH", _c_sz), ("tapsX", ctypes.c_int), ("tapsY", ctypes.c_int),
                 ("phasesX", ctypes.c_int), ("phasesY", ctypes.c_int), ("kernel", ctypes.c_int),
-                ("bandsPerFrame", ctypes.c_int)]
+                ("bandsPerFrame", ctypes.c_int), ("tileRows", ctypes.c_int)]
 
 
 class IpcHandle(ctypes.Structure):
@@ -64,6 +64,7 @@ def lib():
     L.iqo_hip_plan_destroy.argtypes = [_vp]
     L.iqo_hip_plan_destroy.restype = None
     L.iqo_hip_plan_query.argtypes = [_vp, ctypes.POINTER(PlanDesc)]
+    L.iqo_hip_plan_prepare.argtypes = [_vp]
     L.iqo_hip_plan_set_option.argtypes = [_vp, ctypes.c_char_p, ctypes.c_long]
     L.iqo_hip_resize.argtypes = [_vp, _c_sz, _vp, _c_sz, _vp]
     L.iqo_hip_resize_device.argtypes = [_vp, _c_sz, _c_sz, _c_sz, _vp, _c_sz, _c_sz, _vp, _vp]
@@ -223,12 +224,16 @@ class _Resizer:
     def set_option(self, key, value):
         _check(lib().iqo_hip_plan_set_option(self._plan, key.encode(), int(value)), "set_option")
 
+    def prepare(self):
+        """Upload the device tables now (before graph capture / async-only use)."""
+        _check(lib().iqo_hip_plan_prepare(self._plan), "prepare")
+
     def describe(self):
         d = PlanDesc()
         _check(lib().iqo_hip_plan_query(self._plan, ctypes.byref(d)), "query")
         return {"method": d.method, "device": d.device, "tapsX": d.tapsX, "tapsY": d.tapsY,
                 "phasesX": d.phasesX, "phasesY": d.phasesY, "kernel": KERNELS.get(d.kernel, d.kernel),
-                "bands": d.bandsPerFrame}
+                "bands": d.bandsPerFrame, "tile_rows": d.tileRows}
 
     # -- torch convenience: src [F, srcH, srcW] (or [srcH, srcW]) uint8 on the plan's device
     def resize_tensor(self, src, out=None, stream=None):

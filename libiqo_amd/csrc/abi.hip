@@ -65,6 +65,7 @@ struct iqo_hip_plan {
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
     // it off, leaving general_kernel)
     iqo_amd::TileTables tt;
+    int tileTH0 = 0, tileSrcRows0 = 0;  // the auto tile height (option "tile_rows" changes it; reset_options restores it)
     bool useTile = true;
     int4 *dTRows = nullptr, *dTSpans = nullptr;
     int2 *dTCols = nullptr;
@@ -568,6 +569,10 @@ void reset_options(iqo_hip_plan *h)
     h->ratioAlt = 1;
     h->chunkFrames = 0;
     h->useTile = h->useWalk = h->useUp2 = h->useD32 = h->useD31 = h->useRyx = h->useL23 = h->useU23 = h->useA32 = true;
+    if (h->tt.ok) {  // option "tile_rows"
+        h->tt.TH = h->tileTH0;
+        h->tt.srcRows = h->tileSrcRows0;
+    }
 }
 
 // Destroyed plans are kept (options reset) and handed out again for an identical request: the
@@ -651,6 +656,8 @@ int make_plan(iqo_amd::Method m, unsigned degree, size_t sw, size_t sh, size_t d
     }
     h->nChunks = static_cast<int>(chunks.size());
     iqo_amd::build_tile_tables(h->p, &h->tt);
+    h->tileTH0 = h->tt.TH;
+    h->tileSrcRows0 = h->tt.srcRows;
     std::vector<int4> xr = coord_records(h->p.x), yr = coord_records(h->p.y);
     if ((rc = upload(h, &h->dX, xr.data(), xr.size())) || (rc = upload(h, &h->dY, yr.data(), yr.size())) ||
         (rc = upload(h, &h->dTabX, h->p.x.table.data(), h->p.x.table.size())) ||
@@ -1060,9 +1067,10 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->t31.ok && h->useD31 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LANCZOS_D31;
-    // exact vertical ratio, tabled columns: dword loads, 2-byte stores
+    // exact vertical ratio, tabled columns: dword loads; 2-byte stores (1-byte stores when the
+    // destination is not 2-byte aligned, launch_ryx)
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->ryx.ok && h->useRyx &&
-        aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 2, dstSt, dstFrameSt))
+        aligned(src, 4, srcSt, srcFrameSt))
         kernel = IQO_KERNEL_RYX;
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
@@ -1239,7 +1247,18 @@ int iqo_hip_plan_query(const iqo_hip_plan *h, iqo_hip_plan_desc *d)
     d->phasesY = h->p.y.phases;
     d->kernel = plan_kernel(h);
     d->bandsPerFrame = h->bands;
+    d->tileRows = h->tt.ok ? h->tt.TH : 0;
     return IQO_HIP_OK;
+}
+
+int iqo_hip_plan_prepare(iqo_hip_plan *h)
+{
+    if (!h)
+        return IQO_HIP_EINVAL;
+    DeviceGuard guard(h->device);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+    return ensure_tables(h);
 }
 
 int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)

@@ -3004,6 +3004,7 @@ struct RyxArgs {
     int rowBegin, rowEnd, groupBegin, rowsPerBand, bands;
     int srcBytes, dstBytes;
     unsigned nBlocks;
+    int byteStores;  // destination not 2-byte aligned (base or strides): two 1-byte stores per thread
 };
 
 #ifndef IQO_RYX_WPE
@@ -3084,7 +3085,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // interior Lanczos columns divide by 2^20 (magic_x: m = 2^31, shift 19), which is one
     // saturating pack of both columns; only the few border columns take the exact division
     const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
-    const int stoff = x0 < xHi && IQO_RYX_EXP != 2 ? x0 : OOB;  // part bounds are even (launch_ryx)
+    // part bounds are even (launch_ryx) except an odd output width's end: its last thread has one
+    // column and stores one byte (so does every thread, twice, when the destination is not 2-byte
+    // aligned); uniform per workgroup
+    const bool pair = x0 + 1 < xHi;
+    const bool bytes = a.byteStores != 0, oddEnd = (xHi & 1) != 0;
+    const int stoff = x0 < xHi && (pair || bytes) && IQO_RYX_EXP != 2 ? x0 : OOB;
+    const int stoff1 = bytes ? (pair && IQO_RYX_EXP != 2 ? x0 + 1 : OOB) : (x0 < xHi && !pair ? x0 : OOB);
 
     // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1.
     // Rows outside the image load as zero (the reference's masked border sums); rows past the
@@ -3235,8 +3242,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
                 packed = opaque(static_cast<uint32_t>(o[0])) | (opaque(static_cast<uint32_t>(o[1])) << 8);
             }
             const bool ok = y >= y0 && y < y1;
-            __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(packed), dstR,
-                                                  stoff + (ok ? (y - dstRow0) * dstSt : OOB), 0, 0);
+            const int rowOff = ok ? (y - dstRow0) * dstSt : OOB;
+            if (bytes) {
+                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff + rowOff, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed >> 8), dstR, stoff1 + rowOff, 0, 0);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(packed), dstR, stoff + rowOff, 0, 0);
+                if (oddEnd)
+                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff1 + rowOff, 0, 0);
+            }
             if constexpr (!PIPE)
                 next_vertical();
         });
@@ -4118,7 +4132,7 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    if (d.srcW % 4 || d.srcW > 2048 || d.dstW > 1024 || d.dstW % 2)
+    if (d.srcW % 4 || d.srcW > 2048 || d.dstW > 1024)
         return hipErrorInvalidValue;
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
@@ -4175,8 +4189,11 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames) * static_cast<uint64_t>(d.parts);
     if (nBlocks >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
+    // 2-byte stores need an even destination base and even strides; otherwise 1-byte stores
+    const int byteStores = ((reinterpret_cast<uintptr_t>(io.dst) | static_cast<uintptr_t>(io.dstSt) |
+                             static_cast<uintptr_t>(io.dstFrameSt)) & 1) != 0;
     RyxArgs a{d, io, rowBegin, rowEnd, groupBegin, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
-              static_cast<unsigned>(nBlocks)};
+              static_cast<unsigned>(nBlocks), byteStores};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(static_cast<unsigned>(threads)), args,
                            static_cast<size_t>(ldsBytes), s);

@@ -195,8 +195,12 @@ int main(int argc, char **argv)
             rc = EIO;
         }
     }
+    const bool usedYuv = yuv != nullptr;
     if (yuv)
         iqo_hip_yuv_plan_destroy(yuv);
+    int onHip = 0, onCpu = 0;
+    iqo_dropin_backend_counts(&onHip, &onCpu);
+    std::printf("backend: hip %d cpu %d (YUV420 plan: %s)\n", onHip, onCpu, usedYuv ? "yes" : "no");
     std::fclose(in);
     if (std::fclose(out) != 0 && rc == 0)
         rc = EIO;

@@ -10,6 +10,7 @@
 // benchmark.cpp:215-226) and comparing with its solo output.  Exit status 0 = every concurrent
 // output byte-identical to the solo one; each job's solo output and input go to OUT_DIR for the
 // Python test to check against the Generic oracle.
+#include <iqo_hip.h>
 #include <libiqo/iqo.hpp>
 
 #include <atomic>
@@ -103,6 +104,9 @@ int main(int argc, char **argv)
         for (auto &x : th)
             x.join();
     }
+    int onHip = 0, onCpu = 0;
+    iqo_dropin_backend_counts(&onHip, &onCpu);
     std::printf("threads %d rounds %d mismatches %d\n", nThreads, rounds, bad.load());
+    std::printf("backend: hip %d cpu %d\n", onHip, onCpu);
     return bad.load() ? 1 : 0;
 }

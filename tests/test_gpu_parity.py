@@ -4,6 +4,7 @@ bit-exactly.  Checkers: the golden vectors from the reference (tests/golden) and
 sizes, size-independent properties are checked too (fast kernel == general kernel on the same
 batch, band-sharded == unsharded, flat stays flat).  All tests run in one process."""
 import base64
+import os
 
 import numpy as np
 import pytest
@@ -19,6 +20,18 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
 import libiqo_amd  # noqa: E402
 
 DEV = torch.device("cuda:0")
+# Every drop-in C++ object in this process and in the tools these tests start (they inherit the
+# environment) must run on the HIP backend: any CPU fallback aborts (libiqo_amd/csrc/resizers.cpp).
+os.environ["IQO_REQUIRE_HIP"] = "1"
+
+
+def _backend(stdout):
+    """The "backend: hip H cpu C" line the drop-in tools print (iqo_dropin_backend_counts)."""
+    for line in stdout.splitlines():
+        t = line.split()
+        if t[:1] == ["backend:"] and t[1] == "hip" and t[3] == "cpu":
+            return int(t[2]), int(t[4])
+    raise AssertionError("no backend line in:\n" + stdout)
 
 
 def _expected(c):
@@ -611,6 +624,8 @@ def test_cpp_dropin_benchmark_cli(tmp_path, m, iw, ih, ow, oh):
                         "-cycles", "2", "-check", str(out)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ms/cycle" in r.stdout
+    hip, cpu = _backend(r.stdout)
+    assert hip >= 6 and cpu == 0, r.stdout  # 3 objects per cycle, 2 cycles, all on HIP
     got = np.fromfile(str(out), dtype=np.uint8).reshape(oh, ow)
     method = "lanczos" if m.startswith("lanczos") else m
     degree = int(m[7]) if method == "lanczos" else 0
@@ -638,6 +653,8 @@ def test_sample_yuv420p_file_tool(tmp_path, m, iw, ih, ow, oh):
     r = subprocess.run([exe, "-m", m, "-i", str(fin), "-iw", str(iw), "-ih", str(ih), "-o", str(fout),
                         "-ow", str(ow), "-oh", str(oh), "-frames", "2"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+    hip, cpu = _backend(r.stdout)
+    assert cpu == 0 and (hip == 3 or "YUV420 plan: yes" in r.stdout), r.stdout
     got = np.fromfile(str(fout), dtype=np.uint8)
     assert got.size == 2 * ndst
     method = "lanczos" if m.startswith("lanczos") else m
@@ -679,8 +696,10 @@ def test_reference_sample_binary_on_gpu(tmp_path, m, iw, ih, ow, oh):
     fin, fout = tmp_path / "in.yuv", tmp_path / "out.yuv"
     raw.tofile(str(fin))
     r = subprocess.run([exe, "-m", m, "-i", str(fin), "-iw", str(iw), "-ih", str(ih), "-o", str(fout),
-                        "-ow", str(ow), "-oh", str(oh)], capture_output=True, text=True, timeout=120)
+                        "-ow", str(ow), "-oh", str(oh)], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, IQO_DROPIN_REPORT="1"))
     assert r.returncode == 0, r.stdout + r.stderr
+    assert "libiqo_amd drop-in: objects hip=3 cpu=0, resize calls hip=3 cpu=0" in r.stderr, r.stderr
     got = np.fromfile(str(fout), dtype=np.uint8)
     assert got.size == ndst
     method = "lanczos" if m.startswith("lanczos") else m
@@ -695,18 +714,30 @@ def test_reference_sample_binary_on_gpu(tmp_path, m, iw, ih, ow, oh):
         assert (dc == exp).all(), (m, p)
 
 
-def test_reference_benchmark_binary_on_gpu():
+@pytest.mark.parametrize("m,iw,ih,ow,oh", [("lanczos3", 3840, 2160, 1920, 1080), ("lanczos2", 640, 480, 320, 240)])
+def test_reference_benchmark_binary_on_gpu(tmp_path, m, iw, ih, ow, oh):
     """The reference's own benchmark/benchmark.cpp, compiled unchanged against the drop-in, runs
-    its 256-cycle timed loop (resizers constructed inside the loop) on the GPU backend."""
-    import os
+    its 256-cycle timed loop (resizers constructed inside the loop) on the GPU backend: every
+    object and every resize() call on HIP (IQO_DROPIN_REPORT), and the pixels of its first cycle
+    (IQO_DROPIN_DUMP: Y, U, V) equal to the Generic oracle on the benchmark's own input
+    (std::mt19937(0) per plane, benchmark.cpp:51-59,1013-1015; chroma at pxScale 2, :206-229)."""
     import subprocess
     exe = os.path.join(_DROPIN, "benchmark")
     if not os.path.exists(exe):
         pytest.skip("reference tools not built")
-    r = subprocess.run([exe, "-m", "lanczos3", "-iw", "3840", "-ih", "2160", "-ow", "1920", "-oh", "1080"],
-                       capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, "-m", m, "-iw", str(iw), "-ih", str(ih), "-ow", str(ow), "-oh", str(oh)],
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, IQO_DROPIN_REPORT="1", IQO_DROPIN_DUMP=str(tmp_path)))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "elapsed time" in r.stdout and "ms/cycle" in r.stdout
+    assert "size: %dx%d" % (iw, ih) in r.stdout and "size: %dx%d" % (ow, oh) in r.stdout
+    assert "objects hip=512 cpu=0, resize calls hip=768 cpu=0" in r.stderr, r.stderr  # 256 cycles x (1 + 1) objects, 3 calls
+    degree = int(m[7])
+    planes = [(0, iw, ih, ow, oh, 1), (1, iw // 2, ih // 2, ow // 2, oh // 2, 2), (2, iw // 2, ih // 2, ow // 2, oh // 2, 2)]
+    for k, sw, sh, dw, dh, px in planes:
+        got = np.fromfile(str(tmp_path / ("resize%d_%dx%d.raw" % (k, dw, dh))), np.uint8).reshape(dh, dw)
+        exp = ol.run_oracle("lanczos", degree, sw, sh, dw, dh, px, ol.gen("mt19937", sw, sh, 0))
+        assert (got == exp).all(), (m, k)
 
 
 def test_concurrent_plans_from_host_threads(tmp_path):
@@ -720,6 +751,8 @@ def test_concurrent_plans_from_host_threads(tmp_path):
     exe = os.path.join(os.path.dirname(libiqo_amd.LIB_PATH), "build", "threads_test")
     r = subprocess.run([exe, str(tmp_path), "12", "3"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
+    hip, cpu = _backend(r.stdout)
+    assert hip == 48 and cpu == 0, r.stdout  # 12 solo + 3 x 12 concurrent objects
     jobs = sorted(glob.glob(str(tmp_path / "*.src")))
     assert len(jobs) == 12
     for sp in jobs:
@@ -1145,6 +1178,9 @@ RYX_SHAPES = [
     ("lanczos", 3, 1280, 720, 570, 320, 1),
     ("lanczos", 2, 720, 576, 1000, 256, 1),      # columns upscaled
     ("area", 0, 720, 576, 360, 256, 1),
+    ("lanczos", 3, 1920, 1080, 853, 480, 1),     # odd output width: the last column's 1-byte store
+    ("area", 0, 1920, 1080, 853, 480, 1),
+    ("lanczos", 2, 1280, 720, 569, 320, 1),
 ]
 
 
@@ -1198,6 +1234,18 @@ def test_ryx_matches_oracle(cfg):
     r.resize_device(n, sw, sh * sw, src.data_ptr(), dw + 1, dh * (dw + 1), dst.data_ptr())
     torch.cuda.synchronize()
     assert (dst[:, :, :dw].cpu().numpy() == out).all(), cfg
+    # the host-pointer entry point (the reference's resize()): the kernel the host picks for the
+    # shape and its result, one frame, tight destination rows (odd widths: odd stride)
+    assert libiqo_amd.host_kernel_for(m, d, sw, sh, dw, dh, px) == "ryx"
+    hout = np.full((dh, dw), 7, np.uint8)
+    r.resize(sw, np.ascontiguousarray(frames[0]), dw, hout)
+    assert (hout == exp[0]).all(), (cfg, "host path")
+    # destination base not 2-byte aligned (1-byte stores)
+    obuf = torch.full((n * dh * dw + 1,), 5, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sw, sh * sw, src.data_ptr(), dw, dh * dw, obuf.data_ptr() + 1)
+    torch.cuda.synchronize()
+    ob = obuf.cpu().numpy()
+    assert ob[0] == 5 and (ob[1:].reshape(n, dh, dw) == out).all(), (cfg, "odd base")
 
 
 STACK_SHAPES = [
@@ -1281,8 +1329,12 @@ def test_plan_cache_resets_options():
     exp = ol.run_oracle("lanczos", 3, sw, sh, dw, dh, 1, frame)
     r = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh)
     default_kernel = r.describe()["kernel"]
+    default_rows = r.describe()["tile_rows"]
+    assert default_rows > 0
     r.set_option("force_general", 1)
     r.set_option("bands", 3)
+    r.set_option("tile_rows", 1 if default_rows != 1 else 2)
+    assert r.describe()["tile_rows"] != default_rows
     assert r.describe()["kernel"] == "general"
     del r
     import gc
@@ -1290,6 +1342,8 @@ def test_plan_cache_resets_options():
     for _ in range(3):
         r2 = libiqo_amd.LanczosResizer(3, sw, sh, dw, dh)
         assert r2.describe()["kernel"] == default_kernel
+        assert r2.describe()["tile_rows"] == default_rows
+        r2.prepare()  # eager table upload (iqo_hip_plan_prepare): idempotent, then the resize
         assert (_run_host(r2, frame, dw, dh) == exp).all()
         del r2
         gc.collect()

@@ -71,7 +71,8 @@ def _shapes():
            ("lanczos_d31", "lanczos", 3, 1932, 1083, 644, 361),
            ("ryx", "lanczos", 3, 1920, 1080, 854, 480), ("ryx", "lanczos", 2, 1920, 1080, 854, 480),
            ("ryx", "area", 0, 1920, 1080, 854, 480), ("ryx", "lanczos", 3, 1920, 1080, 640, 480),
-           ("ryx", "lanczos", 3, 1280, 720, 570, 320), ("ryx", "area", 0, 720, 576, 360, 256)]
+           ("ryx", "lanczos", 3, 1280, 720, 570, 320), ("ryx", "area", 0, 720, 576, 360, 256),
+           ("ryx", "lanczos", 3, 1920, 1080, 853, 480), ("ryx", "area", 0, 1920, 1080, 853, 480)]  # odd widths
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -83,7 +84,7 @@ def _shapes():
         out.append(("lanczos_d31", "lanczos", rng.choice((2, 3)), 12 * a + 48, 3 * b + 24, 4 * a + 16, b + 8))
         sw = 4 * rng.randint(20, 500)
         out.append(("ryx", rng.choice(("lanczos", "area")), 3, sw, 9 * b + 36,
-                    2 * rng.randint(sw // 4 + 1, min(1024, sw) // 2), 4 * b + 16))
+                    2 * rng.randint(sw // 4 + 1, min(1024, sw) // 2) - rng.randint(0, 1), 4 * b + 16))
     return out
 
 
