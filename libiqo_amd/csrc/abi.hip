@@ -56,6 +56,7 @@ struct iqo_hip_plan {
     int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
     int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
+    int tail = 0;           // block-shared streamer: short bands for each XCD's last frame (0 auto, -1 off, n bands)
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
@@ -562,6 +563,7 @@ void reset_options(iqo_hip_plan *h)
     h->xcdOrder = 1;
     h->ringPack = 0;
     h->rounds = 0;
+    h->tail = 0;
     h->stack = 1;
     h->ryxSplit = 1;
     h->lanes = 0;
@@ -718,6 +720,7 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.prefetch = h->prefetch;
     l.ringPack = h->ringPack;
     l.rounds = h->rounds;
+    l.tail = h->tail;
     l.stack = h->stack;
     l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
     l.NX = f.NX;
@@ -1275,6 +1278,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
 #endif
+    if (!std::strcmp(key, "tail")) {  // block-shared Lanczos streamer: short tail bands (speed only)
+        if (value < -1 || value > 4096)
+            return IQO_HIP_EINVAL;
+        h->tail = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
     if (!std::strcmp(key, "rounds")) {  // block-shared Lanczos streamer: auto band count (speed only)
         if (value < -1 || value > 64)
             return IQO_HIP_EINVAL;

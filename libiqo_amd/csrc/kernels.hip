@@ -545,6 +545,10 @@ struct LanczosArgs {
     int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
     int lastLanes;           // block-shared streamer: lanes of the last DMA chunk (0 = all 64)
     int fpw, frames;         // frame-stacked streamer: frames per workgroup, frames in the launch
+    // block-shared streamer, XCD tail split (tailBands > 0): XCD x takes frames [x F8, (x+1) F8),
+    // all but the last in `bands` bands of rowsPerBand rows, the last in tailBands bands of
+    // tailRows rows, in that order; grid.x = 8 ((F8 - 1) bands + tailBands)
+    int tailBands, tailRows, framesPerXcd;
 };
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
@@ -811,6 +815,35 @@ __device__ __forceinline__ void dma_row_masked(uint32_t lds, int voff, __amdgpu_
                  : "memory");
 }
 
+#ifndef IQO_SYMB_EDGE_BATCH
+#define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (narrow-row scheme; C2 before the line scheme: 64 -> 16 cut write traffic +4.5% -> +2%)
+#endif
+#ifndef IQO_SYMB_NT
+#define IQO_SYMB_NT 2  // block-shared streamer cache policy: nontemporal DMA loads (1) / stores (2); stores
+                       // by default (C2 x256: 0.549 -> 0.544 ms at 24 bands, 0.531 -> 0.520 at 96; nontemporal
+                       // loads lose the halo rows neighbouring bands share in L2: 0.560)
+#endif
+// The block-shared streamer's border-column scheme: whole 128-byte pieces parked and stored once per
+// trip (rows of >= 256 outputs with >= 16 producing lanes per wave), else the divided bytes stored
+// over the row (narrow rows)
+inline __host__ __device__ bool symb_line(int dstW, int np) { return dstW >= 256 && np >= 16; }
+// LDS bytes of the block-shared streamer's edge area (after the ring): the line scheme's parked
+// pieces and sums of one trip of NY/2 rows, or the narrow-row scheme's sums
+constexpr int symb_edge_bytes(int NY)
+{
+    return 2 * (NY / 2) * (128 + 16) > 2 * IQO_SYMB_EDGE_BATCH * 16 ? 2 * (NY / 2) * (128 + 16)
+                                                                     : 2 * IQO_SYMB_EDGE_BATCH * 16;
+}
+__device__ __forceinline__ void dma_row_nt(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff)
+{
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                 "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
+                 : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
 {
@@ -1063,11 +1096,9 @@ __global__ __launch_bounds__(256, 4) void lanczos_sym_kernel(LanczosArgs a)
 #define IQO_SYMB_EXP 0  // timing experiments in variant builds (wrong output): 1 no vertical MACs,
                         // 2 half the horizontal dots, 3 / 4 dot2 / dot4 in place of the MACs
 #endif
-#ifndef IQO_SYMB_EDGE_BATCH
-#define IQO_SYMB_EDGE_BATCH 16  // rows of border-column sums parked before a flush (C2: 64 -> 16 cuts write traffic +4.5% -> +2%)
-#endif
-template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
-__device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by)
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, bool LINE>
+__device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, const unsigned bx, const unsigned by,
+                                                         const int rpb)
 {
     constexpr int H = NY / 2;                   // symmetric pairs = iterations per window cycle
     static_assert(NY % 2 == 0 && NX % 2 == 0 && (OFFX & 1), "even taps, odd first X column");
@@ -1083,15 +1114,19 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     constexpr int JLO = (OFFX + 1) / 2;         // output k, pair p reads Q_{k + p + JLO}
     constexpr int JHI = 7 + NX / 2 + JLO;       // one past the last pair index read
     static_assert(JLO >= -7 && JHI <= 17, "horizontal taps must stay within the neighbouring lanes");
-    // LDS: ring [K slots][2 rows][rowPitch] | edgeSum int4 [2][EDGE_BATCH] | 1 KiB DMA sink (only
-    // when some wave has fewer chunks than CPW)
+    // LDS: ring [K slots][2 rows][rowPitch] | edge area (symb_edge_bytes) | 1 KiB DMA sink (only
+    // when some wave has fewer chunks than CPW).  Edge area: line scheme [2][H][128] parked bytes +
+    // int4 [2][H] border sums; narrow rows int4 edgeSum [2][EDGE_BATCH]
     constexpr int EB = IQO_SYMB_EDGE_BATCH;
     static_assert((EB & (EB - 1)) == 0 && EB <= 64, "edge batch: power of two <= 64");
+    static_assert(H <= 8, "line-scheme flush: 4 rows per 8-B store, two stores");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int rowPitch = a.rowPitch, slotBytes = 2 * rowPitch;
     uint8_t *const ring = lds;
     int4 (*const edgeSum)[EB] = reinterpret_cast<int4 (*)[EB]>(lds + K * slotBytes);
-    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + 2 * EB * 16);
+    uint8_t *const lineBuf = lds + K * slotBytes;                                      // [2][H][128]
+    int4 *const lineSum = reinterpret_cast<int4 *>(lds + K * slotBytes + 2 * H * 128); // [2][H]
+    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + symb_edge_bytes(NY));
     // the last chunk of a row DMAs only its first lastLanes lanes (the row's pitch ends there)
     const int lastLanes = a.lastLanes > 0 && a.lastLanes < 64 ? a.lastLanes : 64;
     const uint64_t lastMask = lastLanes == 64 ? ~0ull : (1ull << lastLanes) - 1ull;
@@ -1101,8 +1136,8 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const int wpr = a.wavesPerRow;                 // = waves of this workgroup
     const int band = static_cast<int>(bx), wcol = wib;
-    const int y0 = a.rowBegin + band * a.rowsPerBand;
-    const int y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    const int y0 = a.rowBegin + band * rpb;  // rpb: rows per band of this workgroup's band size
+    const int y1 = min(y0 + rpb, a.rowEnd);
     if (y0 >= y1)
         return;  // whole workgroup
 
@@ -1115,6 +1150,19 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const int ldsCol = lane <= np + 1 ? 16 + cb : 0;  // this lane's 16 bytes in an LDS ring row
     const bool edgeL = x0 == 0 && !(IQO_DBG(a) & 4), edgeR = x0 + opw >= L.dstW && !(IQO_DBG(a) & 4);
     const bool laneL = outX == 0, laneR = outX == L.dstW - 8;
+    // Border columns, line scheme (rows of >= 256 outputs, >= 16 producing lanes): the lanes holding
+    // the row's first and last 128 output bytes (the edge lanes among them) do not store; they park
+    // their 8 bytes per row in LDS, the edge lane also its 4 raw border sums, and once per trip of H
+    // rows one pass divides the sums into the parked bytes and stores the two 128-byte pieces of
+    // every row whole.  Every output byte is then written once, and a row starting on a 128-B line
+    // (the C2 layout) is written in whole lines: storing the 4 divided bytes over an already written
+    // line (the narrow-row scheme below) cost C2 2.4 % in partial-line writes, and its per-row
+    // parking and flush 7 % of the compute-only time.
+    // (LINE: chosen by the host, symb_line(): dstW >= 256 and >= 16 producing lanes)
+    const bool regL = LINE && edgeL && produce && outX < 128;
+    const bool regR = LINE && edgeR && produce && outX >= L.dstW - 128;
+    // the lane's parking byte offset in lineBuf (slot 0; slot v adds 128 v), -1: does not park
+    const int parkOff = regL ? outX : regR ? H * 128 + outX - (L.dstW - 128) : -1;
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
@@ -1125,7 +1173,8 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const int srcRow0 = a.io.srcRow0;
     const int dbg = IQO_DBG(a);
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
-    const int stoff = (produce && !(dbg & 1)) ? outX : 0x7ff00000;
+    const int stoff = (produce && !(dbg & 1) && !regL && !regR) ? outX : 0x7ff00000;
+    constexpr int STNT = (IQO_SYMB_NT & 2) ? 2 : 0;  // store cache policy (aux: nt)
     // Odd bands walk bottom-up: a band boundary's halo rows are then read by both bands at the
     // same time (both at their start or both at their end) and the second read hits the
     // Infinity Cache instead of HBM.  The window arithmetic is symmetric, so only the row order
@@ -1168,6 +1217,9 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             if (real && c == a.chunks - 1 && lastLanes < 64) {  // uniform
                 dma_row_masked(d0, v, srcR, so0, lastMask);
                 dma_row_masked(d1, v, srcR, so1, lastMask);
+            } else if (IQO_SYMB_NT & 1) {
+                dma_row_nt(d0, v, srcR, so0);
+                dma_row_nt(d1, v, srcR, so1);
             } else {
                 dma_row(d0, v, srcR, so0);
                 dma_row(d1, v, srcR, so1);
@@ -1208,13 +1260,46 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         if (edgeL) {
             const int4 e = edgeSum[0][lane & (EB - 1)];
             const uint32_t w = fix(e.x, 0) | (fix(e.y, 1) << 8) | (fix(e.z, 2) << 16) | (fix(e.w, 3) << 24);
-            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff : 0x7ff00000, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 65) ? rowOff : 0x7ff00000, 0, 0);
         }
         if (edgeR) {
             const int4 e = edgeSum[1][lane & (EB - 1)];
             const uint32_t w = fix(e.x, 4) | (fix(e.y, 5) << 8) | (fix(e.z, 6) << 16) | (fix(e.w, 7) << 24);
-            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 1) ? rowOff + L.dstW - 4 : 0x7ff00000,
+            __builtin_amdgcn_raw_buffer_store_b32(w, dstR, lane < n && !(dbg & 65) ? rowOff + L.dstW - 4 : 0x7ff00000,
                                                   0, 0);
+        }
+    };
+
+    // Line scheme flush of the trip's first n rows (rows yb + dir r): lanes r < n divide row r's
+    // parked border sums into the first (left) / last (right) 4 parked bytes, then 16 lanes per row
+    // store the 128-byte pieces, 4 rows per instruction.  LDS accesses of one wave complete in order.
+    auto flush_lines = [&](int yb, int n) {
+        auto fix = [&](int sv, int k) {
+            const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.xM[k]) >> L.xT[k];
+            return min(qq, 255u);
+        };
+        // the lane index through an opaque register: the per-lane addresses below are recomputed
+        // here instead of being hoisted out of the row loop, where they would stay live beside the
+        // row window (spills)
+        const int lane = static_cast<int>(opaque(static_cast<uint32_t>(threadIdx.x) & 63u));
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            if (!(side ? edgeR : edgeL))
+                continue;  // uniform
+            if (lane < n) {
+                const int4 e = lineSum[side * H + lane];
+                const uint32_t w = fix(e.x, 4 * side) | (fix(e.y, 4 * side + 1) << 8) | (fix(e.z, 4 * side + 2) << 16) |
+                                   (fix(e.w, 4 * side + 3) << 24);
+                *reinterpret_cast<uint32_t *>(lineBuf + (side * H + lane) * 128 + (side ? 124 : 0)) = w;
+            }
+            const int colBase = side ? L.dstW - 128 : 0;
+#pragma unroll
+            for (int r0 = 0; r0 < H; r0 += 4) {
+                const int r = r0 + (lane >> 4), piece = (lane & 15) * 8;
+                const u32x2 val = *reinterpret_cast<const u32x2 *>(lineBuf + (side * H + min(r, H - 1)) * 128 + piece);
+                const int off = r < n && !(dbg & 65) ? (yb + dir * r - a.io.dstRow0) * dstSt + colBase + piece : 0x7ff00000;
+                __builtin_amdgcn_raw_buffer_store_b64(val, dstR, off, 0, STNT);
+            }
         }
     };
 
@@ -1356,8 +1441,20 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
         u32x2 o;
         o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
         o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, 0);
-        if (edgeL || edgeR) {
+        __builtin_amdgcn_raw_buffer_store_b64(o, dstR, stoff, (yy - a.io.dstRow0) * dstSt, STNT);
+        if (LINE && (edgeL || edgeR)) {
+            // line scheme: slot v of the trip (its first row is iteration base, slot 0)
+            if (parkOff >= 0)
+                *reinterpret_cast<u32x2 *>(lineBuf + parkOff + v * 128) = o;
+            if (edgeL && laneL)  // (a wave whose x0 is not 0 can still have a lane at outX == dstW - 8)
+                lineSum[v] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+            if (edgeR && laneR)
+                lineSum[H + v] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+            if (v == H - 1) {  // a band's last, partial trip is flushed after the loop
+                __builtin_amdgcn_wave_barrier();
+                flush_lines(yy - dir * v, H);
+            }
+        } else if (!LINE && (edgeL || edgeR)) {
             // border columns: the edge lane parks its 4 raw sums (k < 4 left, k >= 4 right) in
             // LDS; every EB rows and at the band end one pass divides them, one row per lane
             const int slot = i & (EB - 1);
@@ -1373,14 +1470,39 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     };
     for (int base = 0; base < nRows; base += H)
         static_for<H>([&](auto uc) { row(uc, base); });
+    if (LINE && (edgeL || edgeR) && nRows % H) {
+        // the band's last trip was partial: its nRows % H rows are still parked
+        const int baseLast = nRows - nRows % H;
+        __builtin_amdgcn_wave_barrier();
+        flush_lines(dir > 0 ? y0 + baseLast : y1 - 1 - baseLast, nRows % H);
+    }
 
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
-template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE>
+template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, bool LINE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lanczos_symb_kernel(LanczosArgs a)
 {
     unsigned bx = blockIdx.x, by = blockIdx.y;
-    if (a.xcd) {
+    int rpb = a.rowsPerBand;
+    if (a.tailBands > 0) {
+        // XCD tail split (speed only; blocks are dealt to the XCDs round-robin, so block L runs on
+        // XCD L mod 8 and each XCD takes its blocks in order): XCD x resizes frames [x F8, (x+1) F8)
+        // in order, the last one in short bands, so the workgroups that run last are short and the
+        // XCD's CUs finish together; neighbouring bands of a frame share that XCD's L2 (halo rows)
+        const int x = static_cast<int>(blockIdx.x & 7u), idx = static_cast<int>(blockIdx.x >> 3);
+        const int F8 = a.framesPerXcd, nLong = (F8 - 1) * a.bands;
+        if (idx < nLong) {
+            const int q = idx / a.bands;
+            by = static_cast<unsigned>(x * F8 + q);
+            bx = static_cast<unsigned>(idx - q * a.bands);
+        } else {
+            by = static_cast<unsigned>(x * F8 + F8 - 1);
+            bx = static_cast<unsigned>(idx - nLong);
+            rpb = a.tailRows;
+            if (static_cast<int>(bx) >= a.tailBands)
+                return;
+        }
+    } else if (a.xcd) {
         // XCD-aware order (speed only): the band workgroups of one frame go to one XCD, so the
         // halo rows two neighbouring bands share hit that XCD's L2, and each XCD streams from
         // 1/8 of the batch's address range
@@ -1389,7 +1511,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void l
         by = lg / bands;
         bx = lg - by * bands;
     }
-    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE>(a, bx, by);
+    lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE, LINE>(a, bx, by, rpb);
 }
 
 
@@ -3747,11 +3869,11 @@ struct Yuv3Args {
     unsigned gxY, gxC;  // grid.x of the Y plane / of each chroma plane
 };
 
-template <int NY, int NX, int OFFX, bool ONE>
+template <int NY, int NX, int OFFX, bool ONE, bool LINE>
 struct SymbY {
     static __device__ __forceinline__ void run(const LanczosArgs &a, unsigned bx, unsigned by)
     {
-        lanczos_symb_kernel_body<NY, NX, OFFX, NY / 2, 1, ONE>(a, bx, by);  // ring depth = window period (prep_lanczos)
+        lanczos_symb_kernel_body<NY, NX, OFFX, NY / 2, 1, ONE, LINE>(a, bx, by, a.rowsPerBand);  // ring depth = window period (prep_lanczos)
     }
 };
 template <int NY, int NX, int OFFX, bool ONE>
@@ -4402,11 +4524,14 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     } else if (shared) {
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
-        ldsBytes = K * 2 * rowPitch + 2 * IQO_SYMB_EDGE_BATCH * 16 + (cpw * wpr > chunks ? 1024 : 0);
+        const bool line = symb_line(l.dstW, np);  // border columns: whole-line scheme
+        ldsBytes = K * 2 * rowPitch + symb_edge_bytes(l.NY) + (cpw * wpr > chunks ? 1024 : 0);
         block = 64 * wpr;
+#define IQO_SYMB_L(NY_, NX_, OX_, K_, CPW_, ONE_)                                                       \
+    (line ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, CPW_, ONE_, true>)             \
+          : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, CPW_, ONE_, false>))
 #define IQO_SYMB_K(NY_, NX_, OX_, K_, ONE_)                                                             \
-    (cpw == 1 ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 1, ONE_>)                  \
-              : reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, 2, ONE_>))
+    (cpw == 1 ? IQO_SYMB_L(NY_, NX_, OX_, K_, 1, ONE_) : IQO_SYMB_L(NY_, NX_, OX_, K_, 2, ONE_))
 #define IQO_SYMB(NY_, NX_, OX_, ONE_)                                                                   \
     (K == 3 ? IQO_SYMB_K(NY_, NX_, OX_, 3, ONE_) : K == 4 ? IQO_SYMB_K(NY_, NX_, OX_, 4, ONE_)          \
             : IQO_SYMB_K(NY_, NX_, OX_, 5, ONE_))
@@ -4418,6 +4543,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB
 #undef IQO_SYMB_K
+#undef IQO_SYMB_L
     } else if (l.sym) {
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         if (l.NY == 10 && one)
@@ -4464,7 +4590,18 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
     a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd,
-                    pack ? lastLanes : 64, fpw, io.frames};
+                    pack ? lastLanes : 64, fpw, io.frames, 0, 0, 0};
+    // XCD tail split: each XCD's last frame in short bands (about 8 rows; option "tail"), when
+    // the batch splits evenly over the 8 XCDs into at least 2 frames each
+    if (shared && !stack && l.xcd && l.tail >= 0 && io.frames % 8 == 0 && io.frames >= 16) {
+        const int tb = l.tail > 0 ? min(l.tail, rows) : (rows + 7) / 8;
+        const int tr = (rows + tb - 1) / tb;
+        a.tailBands = (rows + tr - 1) / tr;
+        a.tailRows = tr;
+        a.framesPerXcd = io.frames / 8;
+        if (a.tailBands <= bands)
+            a.tailBands = 0;  // the bands are already short
+    }
     // buffer ranges: the source window spans rows [srcRow0, srcRowEnd) of the frame, the destination
     // band rows [rowBegin, rowEnd); both must be addressable with 31-bit offsets
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + l.srcW;
@@ -4477,6 +4614,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int waves = bands * wpr;
     P->grid = shared ? dim3(static_cast<unsigned>(bands), static_cast<unsigned>(groups))
                        : dim3(static_cast<unsigned>((waves + 3) / 4), static_cast<unsigned>(io.frames));
+    if (a.tailBands > 0)
+        P->grid = dim3(static_cast<unsigned>(8 * ((a.framesPerXcd - 1) * bands + a.tailBands)), 1u);
     P->block = block;
     P->lds = ldsBytes;
     P->kern = kern;
@@ -4618,6 +4757,7 @@ hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const Lanc
     hipError_t e;
     LanczosDev lyGrid = ly;
     lyGrid.stack = 0;  // the fused launch has one (band, frame) grid for all three planes
+    lyGrid.tail = -1;
     if ((e = prep_lanczos(lyGrid, ioY, 0, ly.dstH, 0, &py)) != hipSuccess ||
         (e = prep_lanczos(lc, ioU, 0, lc.dstH, 0, &pu)) != hipSuccess ||
         (e = prep_lanczos(lc, ioV, 0, lc.dstH, 0, &pv)) != hipSuccess)
@@ -4627,13 +4767,14 @@ hipError_t launch_yuv420_lanczos(const LanczosDev &ly, const Io &ioY, const Lanc
     if (pu.kind != 0 || lc.NY != 4 || pu.pd != 3 || py.kind == 0 || py.pd < 3)
         return hipErrorNotSupported;
     const bool one = (ly.cy[0] & 0xffffu) == 1u;
-    const bool shared = py.kind == 1 && py.block == 256 && py.a.chunks <= 4;
+    // (4 waves per row: >= 1488 outputs, so the Y body always takes the line edge scheme)
+    const bool shared = py.kind == 1 && py.block == 256 && py.a.chunks <= 4 && symb_line(py.a.l.dstW, py.a.np);
     const void *kern = nullptr;
     if (ly.NY == 10 && one)
-        kern = shared ? reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymbY<10, 12, -5, true>, RingChroma>)
+        kern = shared ? reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymbY<10, 12, -5, true, true>, RingChroma>)
                       : reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymY<10, 12, -5, true>, RingChroma>);
     else if (ly.NY == 8)
-        kern = shared ? reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymbY<8, 8, -3, false>, RingChroma>)
+        kern = shared ? reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymbY<8, 8, -3, false, true>, RingChroma>)
                       : reinterpret_cast<const void *>(yuv420_lanczos_kernel<SymY<8, 8, -3, false>, RingChroma>);
     else
         return hipErrorNotSupported;

@@ -194,6 +194,8 @@ struct LanczosDev {
     int rounds;                  // block-shared streamer: target rounds of resident workgroups for the
                                  // auto band count (0 = default 6, -1 = one-round makespan model)
     int stack;                   // narrow frames: several frames per workgroup (lanczos_stack_kernel)
+    int tail;                    // block-shared streamer: short bands for each XCD's last frame
+                                 // (0 = auto, -1 = off, n = n bands of that frame)
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
