@@ -61,7 +61,7 @@ struct iqo_hip_plan {
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
-    int ratioAlt = 1;       // 3:2 and 3:1 kernels: odd row bands walk bottom-up (speed only)
+    int ratioAlt = 1;       // 3:2, 3:1 and 2x kernels: odd row bands walk bottom-up (speed only)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
     // it off, leaving general_kernel)
@@ -819,6 +819,7 @@ iqo_amd::Up2Dev up2_dev(const iqo_hip_plan *h)
     d.dstH = h->p.dstH;
     d.NT = u.NT;
     d.np = h->lanes;
+    d.alt = h->ratioAlt;
     d.cy0 = u.cy0;
     d.cx0 = u.cx0;
     std::memcpy(d.cy1, u.cy1, sizeof d.cy1);

@@ -2455,9 +2455,22 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     const int srcLast = a.io.srcRowEnd - 1;
     auto load_row = [&](int r) -> u32x2 {
         const int rc = min(max(r, srcRow0), srcLast);
-        const bool in = r >= 0 && r < u.srcH && r <= rLast;
+        const bool in = r >= 0 && r < u.srcH && r >= rFirst && r <= rLast;
         return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
     };
+    // Odd bands walk bottom-up (u.alt; round 4, as lanczos_d32_kernel): the halo rows two
+    // neighbouring bands share are then read by both at the same time, and the second read hits
+    // L2.  Walk row t is source row rFirst + t top-down, rLast - t bottom-up; step j holds walk rows
+    // j .. j + NT - 1 in both walks, so walking up, step j (k = kHi - 1 - j) finds tap i of the odd
+    // output at walk row j + NT - 1 - i (the taps reversed: c1 below) and the even output's source
+    // row k at walk row j + NT - 1 + OFF instead of j - OFF.
+    const bool up = u.alt && (band & 1);
+    const int wBase = up ? rLast : rFirst, wStep = up ? -1 : 1;
+    auto walk_row = [&](int t) { return wBase + wStep * t; };
+    uint32_t c1[NT];  // odd-output taps in walk order (SGPR selects, once per band)
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+        c1[i] = up ? u.cy1[NT - 1 - i] : u.cy1[i];
     auto widen = [&](u32x2 v, uint32_t (&P)[4]) {
         P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
         P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
@@ -2559,16 +2572,16 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     };
 
     uint32_t R[NW][4];
-    // the window of step kLo without its newest row: rows rFirst .. rFirst + NT - 2 -> slots 0 .. NT - 2
+    // the window of step 0 without its newest row: walk rows 0 .. NT - 2 -> slots 0 .. NT - 2
 #pragma unroll
     for (int i = 0; i < NT - 1; ++i)
-        widen(load_row(rFirst + i), R[i]);
-    // prefetch: step kLo + v adds row rFirst + NT - 1 + v (slot (v + NT - 1) % NW)
+        widen(load_row(walk_row(i)), R[i]);
+    // prefetch: step v adds walk row NT - 1 + v (slot (v + NT - 1) % NW)
     u32x2 pre[NW];
 #pragma unroll
     for (int v = 0; v < NW; ++v) {
         __builtin_amdgcn_sched_barrier(0);
-        pre[v] = load_row(rFirst + NT - 1 + v);
+        pre[v] = load_row(walk_row(NT - 1 + v));
         // the loop's store pattern (two per step), dropped, so the header waits are steady-state
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
@@ -2576,31 +2589,34 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     // and the trip's two flush stores
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
-    for (int base = kLo; base < kHi; base += NW) {
+    const int nSteps = kHi - kLo;
+    for (int base = 0; base < nSteps; base += NW) {
         static_for<NW>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
-            const int k = base + v;
+            const int j = base + v;                      // walk step
+            const int k = up ? kHi - 1 - j : kLo + j;    // source step: output rows 2k, 2k + 1
+            const int slot = up ? 2 * (NW - 1 - v) : 2 * v;  // park slots: row 2k - (the trip's lowest row)
             __builtin_amdgcn_sched_barrier(0);
-            widen(pre[v], R[(v + NT - 1) % NW]);  // row k + OFF + NT - 1
-            pre[v] = load_row(k + NW + OFF + NT - 1);
+            widen(pre[v], R[(v + NT - 1) % NW]);  // walk row j + NT - 1
+            pre[v] = load_row(walk_row(j + NW + NT - 1));
             uint32_t Wk[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q)  // output row 2k: the source row k itself
-                Wk[q] = pk_mul(R[(v - OFF) % NW][q], u.cy0);
+                Wk[q] = pk_mul(up ? R[(v + NT - 1 + OFF) % NW][q] : R[(v - OFF) % NW][q], u.cy0);
             border_row(Wk, 2 * k);
-            emit(Wk, 2 * k, 2 * v);
+            emit(Wk, 2 * k, slot);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {  // output row 2k + 1: rows k + OFF .. k + OFF + NT - 1
-                uint32_t acc = pk_mul(R[v % NW][q], u.cy1[0]);
+            for (int q = 0; q < 4; ++q) {  // output row 2k + 1: walk rows j .. j + NT - 1
+                uint32_t acc = pk_mul(R[v % NW][q], c1[0]);
 #pragma unroll
                 for (int i = 1; i < NT; ++i)
-                    acc = pk_mad(R[(v + i) % NW][q], u.cy1[i], acc);
+                    acc = pk_mad(R[(v + i) % NW][q], c1[i], acc);
                 Wk[q] = acc;
             }
             border_row(Wk, 2 * k + 1);
-            emit(Wk, 2 * k + 1, 2 * v + 1);
+            emit(Wk, 2 * k + 1, slot + 1);
         });
-        flush(2 * base);
+        flush(up ? 2 * (kHi - NW - base) : 2 * (kLo + base));
     }
 }
 
@@ -4579,8 +4595,15 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             // (C2 x128: 8 bands 0.305 ms, 24 0.296, 48 0.294): workgroups that start and finish at
             // different times spread their requests over the memory channels, and the halo rows of
             // neighbouring bands (same XCD) come from L2
+            // Round 4: and bands of at most ~22 rows for 1920-wide outputs, up to 48 for narrower ones
+            // (C2 x256: 24 bands 0.525 ms, 48 0.510, 96 0.515, 135 0.530; C1 x4096 (320 columns):
+            // 2 bands 0.385, 5 0.366, 10 0.378).  Shorter bands keep the concurrently read source
+            // window compact; longer ones pay less per-band prologue, which weighs more on narrow rows.
             const int64_t want = static_cast<int64_t>(l.rounds > 0 ? l.rounds : 6) * (resident / wpr);
-            bands = static_cast<int>(std::min<int64_t>((want + io.frames - 1) / io.frames, std::max(1, rows / 16)));
+            const int64_t byRounds = (want + io.frames - 1) / io.frames;
+            const int rowsMax = std::min(48, std::max(22, 22 * 1920 / std::max(1, l.dstW)));
+            bands = static_cast<int>(std::min<int64_t>(std::max<int64_t>(byRounds, (rows + rowsMax - 1) / rowsMax),
+                                                       std::max(1, rows / 16)));
         } else {
             bands = choose_bands(rows, io.frames, wpr, resident, l.NY - 2);
         }

@@ -78,6 +78,7 @@ struct Up2Dev {
     int m0, m1;                  // main rows; the others are masked border rows divided by
     uint32_t yM[2][8];           //   magic_y (top: row y, bottom: row y - m1)
     int yS[2][8];
+    int alt;                     // odd row bands walk bottom-up (speed only)
 };
 hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

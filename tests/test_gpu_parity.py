@@ -798,9 +798,11 @@ def test_lanczos_up2_matches_oracle(cfg):
     assert w.describe()["kernel"] == "walk"
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
     for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("lanes", 5), ("lanes", 62)):
-        b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
-        b.set_option(opt, val)
-        assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val)
+        for alt in (1, 0):  # odd bands walking bottom-up (default) / every band top-down
+            b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+            b.set_option(opt, val)
+            b.set_option("ratio_alt", alt)
+            assert (b.resize_tensor(src).cpu().numpy() == out).all(), (cfg, opt, val, alt)
     # row bands through their source windows (odd band edges)
     got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
     cuts = [0, 3, dh // 3 + 1, dh // 2, dh]
