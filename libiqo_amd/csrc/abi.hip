@@ -457,11 +457,43 @@ std::vector<int4> coord_records(const AxisPlan &a)
 }
 
 // Upload the separable tile kernel's tables (TileRec / TileCol have the int4 / int2 layout).
+iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h);
+
+// Tables of the exact-ratio kernels (most take their coefficients as kernel arguments; ryx has
+// device tables).  Built whether or not the tile tables exist: ryx also serves shapes whose taps
+// exceed the tile kernel's (Lanczos-8/9 2:1).
+int upload_exact(iqo_hip_plan *h)
+{
+    // exact-ratio kernels (no device tables: their coefficients are kernel arguments)
+    iqo_amd::build_up2(h->p, h->wt, &h->ut);
+    iqo_amd::build_d32(h->p, h->wt, &h->dt);
+    iqo_amd::build_d31(h->p, &h->t31);
+    iqo_amd::build_ryx(h->p, &h->ryx);
+    if (h->ryx.ok && ryx_dev(h).parts == 0)
+        h->ryx = iqo_amd::RyxTables();  // no column split fits the workgroup limits
+    if (h->ryx.ok) {
+        std::vector<int4> rc(h->ryx.cols.size() / 4);
+        for (size_t i = 0; i < rc.size(); ++i)
+            rc[i] = make_int4(h->ryx.cols[4 * i], h->ryx.cols[4 * i + 1], h->ryx.cols[4 * i + 2], 0);
+        int rc2 = upload(h, &h->dRyxRowCoef, h->ryx.rowCoef.data(), h->ryx.rowCoef.size());
+        if (!rc2)
+            rc2 = upload(h, &h->dRyxColCoef, h->ryx.colCoef.data(), h->ryx.colCoef.size());
+        if (!rc2)
+            rc2 = upload(h, &h->dRyxCols, rc.data(), rc.size());
+        if (rc2)
+            return rc2;
+    }
+    iqo_amd::build_a32(h->p, &h->at);
+    iqo_amd::build_u23(h->p, &h->vt);
+    iqo_amd::build_l23(h->p, &h->lt);
+    return IQO_HIP_OK;
+}
+
 int upload_tile(iqo_hip_plan *h)
 {
     const iqo_amd::TileTables &t = h->tt;
     if (!t.ok)
-        return IQO_HIP_OK;
+        return upload_exact(h);
     std::vector<int4> rows(t.rows.size()), spans(t.spans.size());
     std::vector<int2> cols(t.cols.size());
     for (size_t i = 0; i < rows.size(); ++i)
@@ -514,26 +546,8 @@ int upload_tile(iqo_hip_plan *h)
         if (rc)
             return rc;
     }
-    // exact-ratio kernels (no device tables: their coefficients are kernel arguments)
-    iqo_amd::build_up2(h->p, h->wt, &h->ut);
-    iqo_amd::build_d32(h->p, h->wt, &h->dt);
-    iqo_amd::build_d31(h->p, &h->t31);
-    iqo_amd::build_ryx(h->p, &h->ryx);
-    if (h->ryx.ok) {
-        std::vector<int4> rc(h->ryx.cols.size() / 4);
-        for (size_t i = 0; i < rc.size(); ++i)
-            rc[i] = make_int4(h->ryx.cols[4 * i], h->ryx.cols[4 * i + 1], h->ryx.cols[4 * i + 2], 0);
-        int rc2 = upload(h, &h->dRyxRowCoef, h->ryx.rowCoef.data(), h->ryx.rowCoef.size());
-        if (!rc2)
-            rc2 = upload(h, &h->dRyxColCoef, h->ryx.colCoef.data(), h->ryx.colCoef.size());
-        if (!rc2)
-            rc2 = upload(h, &h->dRyxCols, rc.data(), rc.size());
-        if (rc2)
-            return rc2;
-    }
-    iqo_amd::build_a32(h->p, &h->at);
-    iqo_amd::build_u23(h->p, &h->vt);
-    iqo_amd::build_l23(h->p, &h->lt);
+    if (int rc = upload_exact(h))
+        return rc;
     // per (row, tap): coefficient splat and the clamped source row it reads
     std::vector<uint2> rowTap(t.rowCoef.size());
     for (size_t y = 0; y < t.rows.size(); ++y)
@@ -745,6 +759,8 @@ iqo_amd::AreaDev area_dev(const iqo_hip_plan *h)
     for (int i = 0; i < (a.KX + 1) / 2; ++i)  // odd KX: the last pair is (c_{KX-1}, 0)
         a.cx[i] = pair16(p.far.cx[2 * i], 2 * i + 1 < a.KX ? p.far.cx[2 * i + 1] : 0);
     a.dstH = p.dstH;
+    a.lin = p.far.lin ? 1 : 0;
+    a.srcH = p.srcH;
     return a;
 }
 
@@ -817,6 +833,7 @@ iqo_amd::Up2Dev up2_dev(const iqo_hip_plan *h)
     d.srcH = h->p.srcH;
     d.dstW = h->p.dstW;
     d.dstH = h->p.dstH;
+    d.F = u.F;
     d.NT = u.NT;
     d.np = h->lanes;
     d.alt = h->ratioAlt;
@@ -894,6 +911,7 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     d.Q = t.Q;
     d.taps = t.taps;
     d.NP = t.NP;
+    d.off = t.off;
     d.m0 = t.m0;
     d.m1 = t.m1;
     std::memcpy(d.yM, t.yM, sizeof d.yM);
@@ -901,24 +919,13 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     d.rowCoef = h->dRyxRowCoef;
     d.cols = h->dRyxCols;
     d.colCoef = h->dRyxColCoef;
-    // Lanczos: two workgroups per row (4 waves each, half the columns) when each half's source
-    // span fits 256 threads x 4 columns: barriers over 4 waves instead of 8 (1080p -> 480p:
-    // Lanczos-2 0.171 vs 0.182 ms, Lanczos-3 0.232 vs 0.239; Area 5 % slower, so not for Area;
-    // profiles/r03/ryx_split.txt; option "ryx_split" = 0: off, 2: four 2-wave workgroups)
-    d.parts = 1;
-    for (int k = 0; k < 5; ++k)
-        d.xs[k] = k == 0 ? 0 : d.dstW;
-    for (int k = 0; k < 4; ++k) {
-        d.cs[k] = 0;
-        d.ce[k] = d.srcW;
-    }
-    const int P = h->ryxSplit >= 2 ? 4 : 2, threads = 512 / P;
-    if (h->ryxSplit && d.lanczos && d.dstW >= 32 * P) {
+    // column split into `n` workgroups of `threads` threads: output columns [xs[k], xs[k+1]) (even,
+    // 2 per thread) from source columns [cs[k], ce[k]) (multiples of 4, 4 per thread)
+    auto split = [&](int n, int threads) -> bool {
         int xs[5], cs[4], ce[4];
-        for (int k = 0; k <= P; ++k)
-            xs[k] = k == 0 ? 0 : k == P ? d.dstW : (k * d.dstW / P + 1) & ~1;  // even (2 outputs per thread)
-        bool ok = true;
-        for (int k = 0; k < P && ok; ++k) {
+        for (int k = 0; k <= n; ++k)
+            xs[k] = k == 0 ? 0 : k == n ? d.dstW : (k * d.dstW / n + 1) & ~1;
+        for (int k = 0; k < n; ++k) {
             int lo = 1 << 30, hi = -(1 << 30);
             for (int x = xs[k]; x < xs[k + 1]; ++x) {
                 const int a = t.cols[static_cast<size_t>(x) * 4] / 2 - iqo_amd::kRyxPad;  // even window start
@@ -926,17 +933,33 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
                 hi = std::max(hi, a + 2 * t.NP);
             }
             cs[k] = k == 0 ? 0 : std::max(0, lo) & ~3;
-            ce[k] = k == P - 1 ? d.srcW : std::min(d.srcW, (hi + 3) & ~3);
-            ok = ce[k] - cs[k] <= 4 * threads && xs[k + 1] - xs[k] <= 2 * threads && (k == 0 || lo >= 0) &&
-                 (k == P - 1 || hi <= d.srcW);
+            ce[k] = k == n - 1 ? d.srcW : std::min(d.srcW, (hi + 3) & ~3);
+            if (ce[k] - cs[k] > 4 * threads || xs[k + 1] - xs[k] > 2 * threads || (k > 0 && lo < 0) ||
+                (k < n - 1 && hi > d.srcW) || xs[k + 1] <= xs[k])
+                return false;
         }
-        if (ok) {
-            d.parts = P;
-            std::copy(xs, xs + P + 1, d.xs);
-            std::copy(cs, cs + P, d.cs);
-            std::copy(ce, ce + P, d.ce);
+        d.parts = n;
+        d.threads = threads;
+        for (int k = 0; k < 5; ++k)
+            d.xs[k] = k <= n ? xs[k] : d.dstW;
+        for (int k = 0; k < 4; ++k) {
+            d.cs[k] = k < n ? cs[k] : 0;
+            d.ce[k] = k < n ? ce[k] : d.srcW;
         }
-    }
+        return true;
+    };
+    // Lanczos: two workgroups per row (4 waves each, half the columns) when each half's source
+    // span fits 256 threads x 4 columns: barriers over 4 waves instead of 8 (1080p -> 480p:
+    // Lanczos-2 0.171 vs 0.182 ms, Lanczos-3 0.232 vs 0.239; Area 5 % slower, so not for Area;
+    // profiles/r03/ryx_split.txt; option "ryx_split" = 0: off, 2: four 2-wave workgroups).  Rows
+    // wider than 512 threads x 4 columns take 2 or 4 parts of 512 threads.  parts = 0: no split
+    // fits (build_plan then drops the kernel).
+    d.parts = 0;
+    d.threads = 512;
+    const int n0 = h->ryxSplit >= 2 ? 4 : 2;
+    if (!(h->ryxSplit && d.lanczos && d.dstW >= 32 * n0 && split(n0, 512 / n0)) && !split(1, 512) &&
+        !split(2, 512))
+        split(4, 512);
     return d;
 }
 
@@ -1025,7 +1048,9 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_LANCZOS_D32;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->t31.ok && h->useD31)
         k = IQO_KERNEL_LANCZOS_D31;
-    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->ryx.ok && h->useRyx)
+    // (ryx also takes shapes whose taps exceed the tile kernel's tables: Lanczos-8/9 2:1)
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE || (k == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
+        h->ryx.ok && h->useRyx)
         k = IQO_KERNEL_RYX;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->at.ok && h->useA32)
         k = IQO_KERNEL_AREA_D32;
@@ -1073,8 +1098,8 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         kernel = IQO_KERNEL_LANCZOS_D31;
     // exact vertical ratio, tabled columns: dword loads; 2-byte stores (1-byte stores when the
     // destination is not 2-byte aligned, launch_ryx)
-    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->ryx.ok && h->useRyx &&
-        aligned(src, 4, srcSt, srcFrameSt))
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE || (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
+        h->ryx.ok && h->useRyx && aligned(src, 4, srcSt, srcFrameSt))
         kernel = IQO_KERNEL_RYX;
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
@@ -1982,13 +2007,14 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     if (h.p.kernel != IQO_KERNEL_GENERAL)
         return h.p.kernel;
     iqo_amd::build_tile_tables(h.p, &h.tt);
-    if (!h.tt.ok)
-        return IQO_KERNEL_GENERAL;
-    iqo_amd::build_walk_tables(h.p, h.tt, &h.wt);
+    if (h.tt.ok)
+        iqo_amd::build_walk_tables(h.p, h.tt, &h.wt);
     iqo_amd::build_up2(h.p, h.wt, &h.ut);
     iqo_amd::build_d32(h.p, h.wt, &h.dt);
     iqo_amd::build_d31(h.p, &h.t31);
     iqo_amd::build_ryx(h.p, &h.ryx);
+    if (h.ryx.ok && ryx_dev(&h).parts == 0)
+        h.ryx = iqo_amd::RyxTables();
     iqo_amd::build_a32(h.p, &h.at);
     iqo_amd::build_u23(h.p, &h.vt);
     iqo_amd::build_l23(h.p, &h.lt);

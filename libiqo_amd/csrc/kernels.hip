@@ -2188,6 +2188,88 @@ __global__ __launch_bounds__(256) void area_int_kernel(AreaArgs a)
     area_int_kernel_body<KX, KYT>(a, blockIdx.x, blockIdx.y);
 }
 
+// ================================================================ Linear at exactly 2:1
+//
+// The reference's Linear resizer at 2:1 (e.g. 3840x2160 -> 1920x1080; plan.cpp
+// pick_fast_linear_down): main output i blends source samples 2i + 1 and 2i + 2 on both axes
+// (IQOLinearResizerImpl_Generic.cpp:210-282 row loop, :366-407 main columns); the first and last
+// rows take the edge source row alone (work = 256 s) and the first and last columns the edge work
+// value alone ((w + 128) >> 8; :227-237, :329-364), in the Area arithmetic (u16 work row,
+// (s + 2^22) >> 23, int16 cast, clamp).  Thread = the 16 source columns [16g, 16g + 16) plus the
+// next aligned dword of an output row's two source rows -> output columns 8g .. 8g + 7 from the
+// odd-aligned work pairs (16g + 2k + 1, 16g + 2k + 2): 8 v_perm and 8 packed MACs per source
+// row, one v_dot2 per output.  The layout of area_int_kernel (area_kind 8).
+__device__ __forceinline__ void linear_d2_body(const AreaArgs &a, const unsigned bx, const unsigned by)
+{
+    const AreaDev &g = a.g;
+    const int64_t gid = static_cast<int64_t>(bx) * blockDim.x + threadIdx.x;
+    const int64_t total = static_cast<int64_t>(a.rowEnd - a.rowBegin) * a.groups;
+    if (gid >= total)
+        return;
+    const int y = a.rowBegin + static_cast<int>(gid / a.groups);
+    const int gcol = static_cast<int>(gid % a.groups);
+    // source rows and their (c, c) splats: edge rows take one row at 256
+    int r0 = 2 * y + 1, r1 = 2 * y + 2;
+    uint32_t c0 = g.cy[0], c1 = g.cy[1];
+    if (y == 0 || y == g.dstH - 1) {
+        r0 = r1 = y == 0 ? 0 : g.srcH - 1;
+        c0 = 0x01000100u;
+        c1 = 0u;
+    }
+    const uint8_t *sf = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt + 16 * gcol;
+    const uint8_t *s0 = sf + static_cast<int64_t>(r0 - a.io.srcRow0) * a.io.srcSt;
+    const uint8_t *s1 = sf + static_cast<int64_t>(r1 - a.io.srcRow0) * a.io.srcSt;
+    // the dword after the 16 columns (the last group: clamped inside the row; its byte then only
+    // feeds the high half of the last pair, which the replicated right column does not use)
+    const int nxt = 16 * gcol + 16 <= g.srcW - 4 ? 16 : g.srcW - 4 - 16 * gcol;
+    const uint4 v0 = *reinterpret_cast<const uint4 *>(s0), v1 = *reinterpret_cast<const uint4 *>(s1);
+    const uint32_t e0 = *reinterpret_cast<const uint32_t *>(s0 + nxt), e1 = *reinterpret_cast<const uint32_t *>(s1 + nxt);
+    // odd-aligned pairs (b1, b2) (b3, b4) ... (b15, e0) of one row
+    auto odd = [](uint4 v, uint32_t e, uint32_t (&q)[8]) {
+        q[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c020c01u);
+        q[1] = __builtin_amdgcn_perm(v.y, v.x, 0x0c040c03u);
+        q[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c020c01u);
+        q[3] = __builtin_amdgcn_perm(v.z, v.y, 0x0c040c03u);
+        q[4] = __builtin_amdgcn_perm(0u, v.z, 0x0c020c01u);
+        q[5] = __builtin_amdgcn_perm(v.w, v.z, 0x0c040c03u);
+        q[6] = __builtin_amdgcn_perm(0u, v.w, 0x0c020c01u);
+        q[7] = __builtin_amdgcn_perm(e, v.w, 0x0c040c03u);
+    };
+    uint32_t q0[8], q1[8], w[8];
+    odd(v0, e0, q0);
+    odd(v1, e1, q1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        w[k] = pk_mad(q1[k], c1, pk_mul(q0[k], c0));  // u16 work pairs (16-bit wrap)
+    uint32_t out[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t sum = udot2(w[k], g.cx[0], 1u << 22);
+        const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(sum) >> 23));
+        out[k] = opaque(u > 255 ? 255u : u);
+    }
+    // replicated edge columns: (w + 128) >> 8 of work column 0 / srcW - 1
+    auto edge = [](uint32_t wv) {
+        const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>((wv & 0xffffu) + 128u) >> 8));
+        return u > 255 ? 255u : static_cast<uint32_t>(u);
+    };
+    if (gcol == 0) {
+        const uint32_t w0 = pk_mad(__builtin_amdgcn_perm(0u, v1.x, 0x0c010c00u), c1,
+                                   pk_mul(__builtin_amdgcn_perm(0u, v0.x, 0x0c010c00u), c0));  // (w0, w1)
+        out[0] = opaque(edge(w0));
+    }
+    if (gcol == a.groups - 1)
+        out[7] = opaque(edge(w[7]));  // low half = work column 16g + 15 = srcW - 1
+    uint8_t *d = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt +
+                 static_cast<int64_t>(y - a.io.dstRow0) * a.io.dstSt + 8 * gcol;
+    *reinterpret_cast<uint2 *>(d) = make_uint2(out[0] | (out[1] << 8) | (out[2] << 16) | (out[3] << 24),
+                                               out[4] | (out[5] << 8) | (out[6] << 16) | (out[7] << 24));
+}
+__global__ __launch_bounds__(256) void linear_d2_kernel(AreaArgs a)
+{
+    linear_d2_body(a, blockIdx.x, blockIdx.y);
+}
+
 
 // ================================================================ exact 2x bilinear streamer
 //
@@ -2405,15 +2487,16 @@ struct Up2Args {
     unsigned nWaves;
 };
 
-template <int NT>
+template <int NT, int F>
 __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
 {
     constexpr int NW = NT;           // register window rows
-    constexpr int H = NT / 2;        // coefficient pairs of an odd output
-    constexpr int OFF = 1 - NT / 2;  // window start relative to x >> 1 (y >> 1)
+    constexpr int H = NT / 2;        // coefficient pairs of a phase 1 .. F-1 output
+    constexpr int OFF = 1 - NT / 2;  // window start relative to x / F (y / F)
+    constexpr int OPL = 8 * F;       // output columns per lane
     constexpr int OOB = 0x7ff00000;
     const Up2Dev &u = a.u;
-    __shared__ int4 park[4][2][2 * NW][4];  // per wave, side, row slot: the edge lane's 16 raw sums
+    __shared__ int4 park[4][2][F * NW][OPL / 4];  // per wave, side, row slot: the edge lane's raw sums
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
@@ -2428,12 +2511,12 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     if (y0 >= y1)
         return;
 
-    const int opw = 16 * a.np;
+    const int opw = OPL * a.np;
     const int x0 = max(0, min(wcol * opw, u.dstW - opw));  // first output column of lane 1
-    const int cb = x0 / 2 - 8 + 8 * lane;
+    const int cb = x0 / F - 8 + 8 * lane;
     const bool produce = lane >= 1 && lane <= a.np;
     const int voff = (lane <= a.np + 1 && cb >= 0 && cb + 8 <= u.srcW) ? cb : OOB;
-    const int stoff = produce ? 2 * cb : OOB;
+    const int stoff = produce ? F * cb : OOB;
     const bool edgeL = x0 == 0, edgeR = x0 + opw >= u.dstW;  // wave holds border columns (uniform)
     const bool laneL = edgeL && lane == 1, laneR = edgeR && lane == a.np;
 
@@ -2445,11 +2528,11 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
 
-    // source steps k: output rows 2k, 2k+1 (those outside [y0, y1) are computed and dropped);
+    // source steps k: output rows F k .. F k + F - 1 (those outside [y0, y1) are computed and dropped);
     // step k reads source rows k + OFF .. k + OFF + NT - 1.  Rows outside the image read as zero
     // (the masked border sums); rows of dropped outputs may lie outside the call's window: clamped
     // (never used).  Out-of-range marks go in the (range-checked) VGPR offset.
-    const int kLo = y0 >> 1, kHi = (y1 + 1) >> 1;
+    const int kLo = y0 / F, kHi = (y1 + F - 1) / F;
     const int rFirst = kLo + OFF;
     const int rLast = kHi - 1 + OFF + NT - 1;
     const int srcLast = a.io.srcRowEnd - 1;
@@ -2467,24 +2550,30 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     const bool up = u.alt && (band & 1);
     const int wBase = up ? rLast : rFirst, wStep = up ? -1 : 1;
     auto walk_row = [&](int t) { return wBase + wStep * t; };
-    uint32_t c1[NT];  // odd-output taps in walk order (SGPR selects, once per band)
+    uint32_t c1[F - 1][NT];  // phase 1 .. F-1 taps in walk order (SGPR selects, once per band)
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
-        c1[i] = up ? u.cy1[NT - 1 - i] : u.cy1[i];
+    for (int j = 0; j < F - 1; ++j)
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            c1[j][i] = up ? u.cy1[j][NT - 1 - i] : u.cy1[j][i];
     auto widen = [&](u32x2 v, uint32_t (&P)[4]) {
         P[0] = __builtin_amdgcn_perm(0u, v.x, 0x0c010c00u);  // (cb, cb+1)
         P[1] = __builtin_amdgcn_perm(0u, v.x, 0x0c030c02u);
         P[2] = __builtin_amdgcn_perm(0u, v.y, 0x0c010c00u);
         P[3] = __builtin_amdgcn_perm(0u, v.y, 0x0c030c02u);  // (cb+6, cb+7)
     };
-    auto store_row = [&](u32x4 o, int voffs, int y, bool ok) {
-        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, voffs + (ok ? (y - dstRow0) * dstSt : OOB), 0,
+    // one lane's OPL bytes of row y: one 16-B store (F = 2), 16 + 8 B (F = 3)
+    auto store_row = [&](const uint32_t (&o)[OPL / 4], int voffs, int y, bool ok) {
+        const int off = voffs + (ok ? (y - dstRow0) * dstSt : OOB);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, dstR, off, 0,
                                                2 /* nt: fresh data G2 0.088 vs 0.1015 ms */);
+        if constexpr (F == 3)
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{o[4], o[5]}, dstR, off + 16, 0, 2);
     };
     // masked border row (uniform, rare): work = int16(n * 64 / deno)
     auto border_row = [&](uint32_t (&W)[4], int y) {
         if (y < u.m0 || y >= u.m1) {
-            const int side = y < u.m0 ? 0 : 1, i = min(max(side ? y - u.m1 : y, 0), 7);
+            const int side = y < u.m0 ? 0 : 1, i = min(max(side ? y - u.m1 : y, 0), 15);
             const uint32_t m = u.yM[side][i];
             const int sh = u.yS[side][i];
 #pragma unroll
@@ -2508,46 +2597,45 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
         for (int e = 0; e < 7; ++e)
             O[e] = __builtin_amdgcn_alignbit(E[e + 1], E[e], 16);
         auto pair = [&](int rel) { return (rel & 1) ? O[(rel - 1) / 2] : E[rel / 2]; };  // low half = column rel
-        int sum[16];
+        int sum[OPL];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            if ((j & 1) == 0) {
-                // on a source column: c * w[cb + j/2] (the pair's high half meets a zero coefficient)
-                sum[j] = sdot2(pair((j >> 1) + 4), u.cx0, 1 << 19);
+        for (int j = 0; j < OPL; ++j) {
+            const int m = j / F, ph = j % F;  // output F (cb + m) + ph
+            if (ph == 0) {
+                // on a source column: c * w[cb + m] (the pair's high half meets a zero coefficient)
+                sum[j] = sdot2(pair(m + 4), u.cx0, 1 << 19);
             } else {
-                const int rel = (j >> 1) + OFF + 4;
+                const int rel = m + OFF + 4;
                 int acc = 1 << 19;
 #pragma unroll
                 for (int q = 0; q < H; ++q)
-                    acc = sdot2(pair(rel + 2 * q), u.cx1[q], acc);
+                    acc = sdot2(pair(rel + 2 * q), u.cx1[ph - 1][q], acc);
                 sum[j] = acc;
             }
         }
-        u32x4 o;
-        o.x = pack_hi(pack_lo(sum[0], sum[1]), sum[2], sum[3]);
-        o.y = pack_hi(pack_lo(sum[4], sum[5]), sum[6], sum[7]);
-        o.z = pack_hi(pack_lo(sum[8], sum[9]), sum[10], sum[11]);
-        o.w = pack_hi(pack_lo(sum[12], sum[13]), sum[14], sum[15]);
+        uint32_t o[OPL / 4];
+#pragma unroll
+        for (int q = 0; q < OPL / 4; ++q)
+            o[q] = pack_hi(pack_lo(sum[4 * q], sum[4 * q + 1]), sum[4 * q + 2], sum[4 * q + 3]);
         store_row(o, stoff, y, y >= y0 && y < y1);
         if (edgeL || edgeR) {  // uniform
             if (laneL || laneR) {
                 int4 *pk = park[wib][laneL ? 0 : 1][slot];
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < OPL / 4; ++q)
                     pk[q] = make_int4(sum[4 * q], sum[4 * q + 1], sum[4 * q + 2], sum[4 * q + 3]);
             }
         }
     };
-    // once per trip: lane r < 2 NW rewrites the edge bytes of row yt + r from the parked sums
+    // once per trip: lane r < F NW rewrites the edge bytes of row yt + r from the parked sums
     auto flush = [&](int yt) {
-        u32x4 oL = {0u, 0u, 0u, 0u}, oR = {0u, 0u, 0u, 0u};
-        const int r = min(lane, 2 * NW - 1);
+        uint32_t oL[OPL / 4] = {}, oR[OPL / 4] = {};
+        const int r = min(lane, F * NW - 1);
         if (edgeL || edgeR) {  // uniform
             __builtin_amdgcn_wave_barrier();
-            auto fix = [&](int side) {
-                uint32_t w[4];
+            auto fix = [&](int side, uint32_t (&w)[OPL / 4]) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < OPL / 4; ++q) {
                     const int4 p = park[wib][side][r][q];
                     const int sv[4] = {p.x, p.y, p.z, p.w};
                     uint32_t b[4];
@@ -2558,18 +2646,18 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
                                    255u);
                     w[q] = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
                 }
-                return u32x4{w[0], w[1], w[2], w[3]};
             };
             if (edgeL)
-                oL = fix(0);
+                fix(0, oL);
             if (edgeR)
-                oR = fix(1);
+                fix(1, oR);
         }
         const int y = yt + lane;
-        const bool ok = lane < 2 * NW && y >= y0 && y < y1;
+        const bool ok = lane < F * NW && y >= y0 && y < y1;
         store_row(oL, edgeL ? 0 : OOB, y, ok);
-        store_row(oR, edgeR ? u.dstW - 16 : OOB, y, ok);
+        store_row(oR, edgeR ? u.dstW - OPL : OOB, y, ok);
     };
+    const uint32_t zeros[OPL / 4] = {};
 
     uint32_t R[NW][4];
     // the window of step 0 without its newest row: walk rows 0 .. NT - 2 -> slots 0 .. NT - 2
@@ -2582,41 +2670,45 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     for (int v = 0; v < NW; ++v) {
         __builtin_amdgcn_sched_barrier(0);
         pre[v] = load_row(walk_row(NT - 1 + v));
-        // the loop's store pattern (two per step), dropped, so the header waits are steady-state
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
+        // the loop's store pattern (F rows per step), dropped, so the header waits are steady-state
+#pragma unroll
+        for (int j = 0; j < F; ++j)
+            store_row(zeros, OOB, 0, false);
     }
-    // and the trip's two flush stores
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, OOB, 0, 0);
+    // and the trip's two flush rows
+    store_row(zeros, OOB, 0, false);
+    store_row(zeros, OOB, 0, false);
     const int nSteps = kHi - kLo;
     for (int base = 0; base < nSteps; base += NW) {
         static_for<NW>([&](auto vc) {
             constexpr int v = decltype(vc)::value;
             const int j = base + v;                      // walk step
-            const int k = up ? kHi - 1 - j : kLo + j;    // source step: output rows 2k, 2k + 1
-            const int slot = up ? 2 * (NW - 1 - v) : 2 * v;  // park slots: row 2k - (the trip's lowest row)
+            const int k = up ? kHi - 1 - j : kLo + j;    // source step: output rows F k .. F k + F - 1
+            const int slot = up ? F * (NW - 1 - v) : F * v;  // park slots: row F k - (the trip's lowest row)
             __builtin_amdgcn_sched_barrier(0);
             widen(pre[v], R[(v + NT - 1) % NW]);  // walk row j + NT - 1
             pre[v] = load_row(walk_row(j + NW + NT - 1));
             uint32_t Wk[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q)  // output row 2k: the source row k itself
+            for (int q = 0; q < 4; ++q)  // output row F k: the source row k itself
                 Wk[q] = pk_mul(up ? R[(v + NT - 1 + OFF) % NW][q] : R[(v - OFF) % NW][q], u.cy0);
-            border_row(Wk, 2 * k);
-            emit(Wk, 2 * k, slot);
+            border_row(Wk, F * k);
+            emit(Wk, F * k, slot);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {  // output row 2k + 1: walk rows j .. j + NT - 1
-                uint32_t acc = pk_mul(R[v % NW][q], c1[0]);
+            for (int ph = 1; ph < F; ++ph) {
 #pragma unroll
-                for (int i = 1; i < NT; ++i)
-                    acc = pk_mad(R[(v + i) % NW][q], c1[i], acc);
-                Wk[q] = acc;
+                for (int q = 0; q < 4; ++q) {  // output row F k + ph: walk rows j .. j + NT - 1
+                    uint32_t acc = pk_mul(R[v % NW][q], c1[ph - 1][0]);
+#pragma unroll
+                    for (int i = 1; i < NT; ++i)
+                        acc = pk_mad(R[(v + i) % NW][q], c1[ph - 1][i], acc);
+                    Wk[q] = acc;
+                }
+                border_row(Wk, F * k + ph);
+                emit(Wk, F * k + ph, slot + ph);
             }
-            border_row(Wk, 2 * k + 1);
-            emit(Wk, 2 * k + 1, slot + 1);
         });
-        flush(up ? 2 * (kHi - NW - base) : 2 * (kLo + base));
+        flush(up ? F * (kHi - NW - base) : F * (kLo + base));
     }
 }
 
@@ -3148,11 +3240,12 @@ struct RyxArgs {
 #ifndef IQO_RYX_WPE
 #define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
 #endif
-template <bool LZ, int P, int Q, int T, int OFF, int NP, int PD>
+template <bool LZ, int P, int Q, int T, int NP, int PD>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
 {
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
-    constexpr int NW = (SPAN + P - 1) / P * P;    // register window rows (whole groups of P)
+    constexpr int NW0 = (SPAN + P - 1) / P * P;   // register window rows (whole groups of P) ...
+    constexpr int NW = ((NW0 / P) * Q) % 2 ? NW0 + P : NW0;  // ... and an even number of rows per trip
     constexpr int U = NW / P;                     // groups per unrolled trip (window slots repeat)
     constexpr int UQ = U * Q;                     // output rows per trip
     constexpr int OOB = 0x7ff00000;
@@ -3235,8 +3328,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // Rows outside the image load as zero (the reference's masked border sums); rows past the
     // band's last window are not loaded.  Rows outside the call's source window (band windows) can
     // only be rows no stored output reads, and read as zero (out-of-range offsets).
-    const int rBase = P * mLo + OFF;
-    const int rLast = P * (mLo + nG - 1) + OFF + SPAN - 1;
+    const int rBase = P * mLo + d.off;
+    const int rLast = P * (mLo + nG - 1) + d.off + SPAN - 1;
     const int qLo = max(0, -rBase), qHi = min(d.srcH - 1, rLast) - rBase;
     const int rowOff0 = (rBase - srcRow0) * srcSt;
     auto load_row = [&](int q) -> uint32_t {
@@ -3294,7 +3387,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
         }
         if (LZ && (y < d.m0 || y >= d.m1)) {
             // masked border row (uniform, rare): rows outside the image read as zero
-            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 7);
+            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 15);
             W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
             W[1] = ydiv2(W[1], d.yM[side][i], d.yS[side][i]);
         }
@@ -3912,6 +4005,12 @@ struct AreaPlane {
         area_int_kernel_body<KX, KYT>(a, bx, by);
     }
 };
+struct LinearD2Plane {
+    static __device__ __forceinline__ void run(const AreaArgs &a, unsigned bx, unsigned by)
+    {
+        linear_d2_body(a, bx, by);
+    }
+};
 struct LinearPlane {
     static __device__ __forceinline__ void run(const LinearArgs &a, unsigned bx, unsigned by)
     {
@@ -4142,12 +4241,15 @@ hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, i
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + u.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + u.dstW;  // stores are relative to dstRow0
     if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24) ||
-        (u.NT != 4 && u.NT != 6) || u.dstW % 16 || u.dstW != 2 * u.srcW || u.dstW < 32)
+        (u.NT != 4 && u.NT != 6) || (u.F != 2 && u.F != 3) || u.dstW % (8 * u.F) || u.dstW != u.F * u.srcW ||
+        u.dstW < 16 * u.F || u.dstH != u.F * u.srcH)
         return hipErrorInvalidValue;
-    const void *kern = u.NT == 6 ? reinterpret_cast<const void *>(lanczos_up2_kernel<6>)
-                                 : reinterpret_cast<const void *>(lanczos_up2_kernel<4>);
+    const void *kern = u.F == 3 ? (u.NT == 6 ? reinterpret_cast<const void *>(lanczos_up2_kernel<6, 3>)
+                                             : reinterpret_cast<const void *>(lanczos_up2_kernel<4, 3>))
+                                : (u.NT == 6 ? reinterpret_cast<const void *>(lanczos_up2_kernel<6, 2>)
+                                             : reinterpret_cast<const void *>(lanczos_up2_kernel<4, 2>));
     // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
-    const int lanes = u.dstW / 16;
+    const int lanes = u.dstW / (8 * u.F);
     int wpr = (lanes + 61) / 62;
     int np = u.np > 0 ? min(u.np, min(62, lanes)) : (lanes + wpr - 1) / wpr;
     wpr = (lanes + np - 1) / np;
@@ -4160,7 +4262,7 @@ hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, i
     const int rows = rowEnd - rowBegin;
     bands = std::max(1, std::min(bands, rows));
     int rpb = (rows + bands - 1) / bands;
-    rpb += rpb & 1;  // even: a band's steps produce whole row pairs
+    rpb = (rpb + u.F - 1) / u.F * u.F;  // a band's steps produce whole groups of F rows
     bands = (rows + rpb - 1) / rpb;
     const uint64_t nWaves = static_cast<uint64_t>(wpr) * bands * static_cast<uint64_t>(io.frames);
     if (nWaves >= (uint64_t(1) << 31))
@@ -4270,33 +4372,47 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    if (d.srcW % 4 || d.srcW > 2048 || d.dstW > 1024)
+    if (d.srcW % 4 || d.srcW > 8192 || d.dstW > 4096)
         return hipErrorInvalidValue;
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
     if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
         return hipErrorInvalidValue;
-    // instantiations (plan.cpp build_ryx kShapes): method, P, Q, taps
+    // instantiations (plan.cpp build_ryx kShapes): method, P, Q, taps (the reference's taps less the
+    // zero outer taps of every phase), column pairs
+    struct Inst {
+        bool lz;
+        int P, Q, T, NP;
+        const void *kern;
+    };
+#define IQO_RYX(LZ_, P_, Q_, T_, NP_) {LZ_, P_, Q_, T_, NP_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, 1>)}
+    static const Inst kInst[] = {
+        IQO_RYX(true, 9, 4, 12, 8), IQO_RYX(true, 9, 4, 12, 10),   // Lanczos-3 9:4 (1080p -> 480p, -> 640x480)
+        IQO_RYX(true, 9, 4, 8, 6), IQO_RYX(true, 9, 4, 8, 7),      // Lanczos-2 9:4
+        IQO_RYX(false, 9, 4, 4, 3),                                // Area 9:4
+        IQO_RYX(true, 4, 1, 14, 13), IQO_RYX(true, 4, 1, 14, 9),   // Lanczos-3 / -2 4:1 (4K -> 960x540)
+        IQO_RYX(true, 2, 1, 4, 3),                                 // Lanczos-1 2:1
+        IQO_RYX(true, 2, 1, 12, 9), IQO_RYX(true, 2, 1, 16, 11),   // Lanczos-4 / -5 2:1
+        IQO_RYX(true, 2, 1, 18, 13), IQO_RYX(true, 2, 1, 20, 15),  // Lanczos-6 / -7 2:1
+        IQO_RYX(true, 2, 1, 22, 17), IQO_RYX(true, 2, 1, 24, 19),  // Lanczos-8 / -9 2:1
+    };
+#undef IQO_RYX
     const void *kern = nullptr;
     int trip = 0;
-    // (Lanczos: the reference's 14 / 10 taps less the two zero outer taps, plan.cpp build_ryx)
-    if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 12 && (d.NP == 8 || d.NP == 10)) {
-        kern = d.NP == 8 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 12, -5, 8, 1>)
-                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 12, -5, 10, 1>);
-        trip = 4 * 2;
-    } else if (d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 8 && (d.NP == 6 || d.NP == 7)) {
-        kern = d.NP == 6 ? reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 8, -3, 6, 1>)
-                         : reinterpret_cast<const void *>(ryx_kernel<true, 9, 4, 8, -3, 7, 1>);
-        trip = 4 * 2;
-    } else if (!d.lanczos && d.P == 9 && d.Q == 4 && d.taps == 4 && d.NP == 3) {
-        kern = reinterpret_cast<const void *>(ryx_kernel<false, 9, 4, 4, 0, 3, 1>);
-        trip = 4 * 2;
-    } else {
+    for (const Inst &k : kInst)
+        if (k.lz == d.lanczos && k.P == d.P && k.Q == d.Q && k.T == d.taps && k.NP == d.NP) {
+            kern = k.kern;
+            const int span = (k.P * (k.Q - 1)) / k.Q + k.T, nw0 = (span + k.P - 1) / k.P * k.P;
+            const int nw = ((nw0 / k.P) * k.Q) % 2 ? nw0 + k.P : nw0;
+            trip = nw / k.P * k.Q * 2;  // (as the kernel: output rows per trip) x 2
+        }
+    if (!kern)
         return hipErrorInvalidValue;
-    }
     if (d.parts != 1 && d.parts != 2 && d.parts != 4)
         return hipErrorInvalidValue;
-    const int threads = 512 / d.parts;
+    const int threads = d.threads > 0 ? d.threads : 512 / d.parts;
+    if (threads % 64 || threads > 512 || threads * d.parts > 2048)
+        return hipErrorInvalidValue;
     int maxSpan = d.srcW;
     if (d.parts > 1) {
         // part k: output columns [xs[k], xs[k+1]) (even bounds, <= 2 per thread), source columns
@@ -4310,6 +4426,8 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
                 return hipErrorInvalidValue;
             maxSpan = std::max(maxSpan, d.ce[k] - d.cs[k]);
         }
+    } else if (d.srcW > 4 * threads || d.dstW > 2 * threads) {
+        return hipErrorInvalidValue;
     }
     const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
     const int groupBegin = rowBegin - rowBegin % d.Q;
@@ -4661,9 +4779,11 @@ hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin
 }
 
 // instantiations of area_int_kernel: <4,4> <2,2> <2,*> <4,*> <8,*> <3,3> <3,*> <6,*>
-constexpr int kAreaKinds = 8;
+constexpr int kAreaKinds = 9;  // kind 8: Linear 2:1 (linear_d2_body)
 int area_kind(const AreaDev &g)
 {
+    if (g.lin)
+        return 8;
     if (g.KX == 3)
         return g.KY == 3 ? 5 : 6;
     if (g.KX == 6)
@@ -4682,7 +4802,8 @@ hipError_t prep_area(const AreaDev &g, const Io &io, int rowBegin, int rowEnd, P
         reinterpret_cast<const void *>(area_int_kernel<4, 4>), reinterpret_cast<const void *>(area_int_kernel<2, 2>),
         reinterpret_cast<const void *>(area_int_kernel<2, 0>), reinterpret_cast<const void *>(area_int_kernel<4, 0>),
         reinterpret_cast<const void *>(area_int_kernel<8, 0>), reinterpret_cast<const void *>(area_int_kernel<3, 3>),
-        reinterpret_cast<const void *>(area_int_kernel<3, 0>), reinterpret_cast<const void *>(area_int_kernel<6, 0>)};
+        reinterpret_cast<const void *>(area_int_kernel<3, 0>), reinterpret_cast<const void *>(area_int_kernel<6, 0>),
+        reinterpret_cast<const void *>(linear_d2_kernel)};
     P->kern = kerns[P->kind];
     return hipSuccess;
 }
@@ -4823,7 +4944,7 @@ hipError_t launch_yuv420_area(const AreaDev &gy, const Io &ioY, const AreaDev &g
     (void)prep_area(gy, ioY, 0, gy.dstH, &py);
     (void)prep_area(gc, ioU, 0, gc.dstH, &pu);
     (void)prep_area(gc, ioV, 0, gc.dstH, &pv);
-    if (py.kind != pu.kind || (py.kind >= 2 && py.kind != 5 && gy.KY != gc.KY))
+    if (py.kind != pu.kind || (py.kind >= 2 && py.kind != 5 && py.kind != 8 && gy.KY != gc.KY))
         return hipErrorNotSupported;
     static const void *const kerns[kAreaKinds] = {
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<4, 4>, AreaArgs>),
@@ -4833,7 +4954,8 @@ hipError_t launch_yuv420_area(const AreaDev &gy, const Io &ioY, const AreaDev &g
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<8, 0>, AreaArgs>),
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<3, 3>, AreaArgs>),
         reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<3, 0>, AreaArgs>),
-        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<6, 0>, AreaArgs>)};
+        reinterpret_cast<const void *>(yuv420_plane_kernel<AreaPlane<6, 0>, AreaArgs>),
+        reinterpret_cast<const void *>(yuv420_plane_kernel<LinearD2Plane, AreaArgs>)};
     return launch_fused3(kerns[py.kind], py, pu, pv, 256, 0, s);
 }
 

@@ -67,17 +67,18 @@ hipError_t launch_walk(const WalkDev &w, const Io &io, int rowBegin, int rowEnd,
 // --- exact 2x Lanczos-2/3 upscale, main rows x middle columns (plan.hpp Up2Tables).
 struct Up2Dev {
     int srcW, srcH, dstW, dstH;
+    int F;                       // factor: 2 or 3 (output y = F k + j takes phase j)
     int NT;                      // taps per axis (4 or 6)
     int np;                      // producing lanes per wave (0 = auto)
-    uint32_t cy0;                // even rows: (c, c) splat of the single tap (the source row itself)
-    uint32_t cy1[6];             // odd rows: (c, c) splats of the NT taps
-    uint32_t cx0;                // even columns: (c, 0) of the single tap
-    uint32_t cx1[3];             // odd columns: int16 coefficient pairs of the NT taps
-    uint32_t xM[2][16];          // edge-lane exact divisions (left / right 16 columns)
-    int xT[2][16];
+    uint32_t cy0;                // phase 0 rows: (c, c) splat of the single tap (the source row itself)
+    uint32_t cy1[2][6];          // phase 1 .. F-1 rows: (c, c) splats of the NT taps
+    uint32_t cx0;                // phase 0 columns: (c, 0) of the single tap
+    uint32_t cx1[2][3];          // phase 1 .. F-1 columns: int16 coefficient pairs of the NT taps
+    uint32_t xM[2][24];          // edge-lane exact divisions (left / right 8 F columns)
+    int xT[2][24];
     int m0, m1;                  // main rows; the others are masked border rows divided by
-    uint32_t yM[2][8];           //   magic_y (top: row y, bottom: row y - m1)
-    int yS[2][8];
+    uint32_t yM[2][16];          //   magic_y (top: row y, bottom: row y - m1)
+    int yS[2][16];
     int alt;                     // odd row bands walk bottom-up (speed only)
 };
 hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
@@ -117,20 +118,23 @@ struct D31Dev {
 hipError_t launch_d31(const D31Dev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
 // Exact vertical ratio, tabled columns (plan.hpp RyxTables): every row and column.
-constexpr int kRyxPadK = 16;     // work-row padding (u16 entries) left of column 0: plan.hpp kRyxPad
+constexpr int kRyxPadK = 24;     // work-row padding (u16 entries) left of column 0: plan.hpp kRyxPad
 struct RyxDev {
     bool lanczos;
     int srcW, srcH, dstW, dstH;
     int P, Q, taps, NP;
+    int off;                     // group m's window starts at source row P m + off
     int m0, m1;                  // Lanczos main rows; the others are masked border rows (magic_y)
-    uint32_t yM[2][8];
-    int yS[2][8];
+    uint32_t yM[2][16];
+    int yS[2][16];
     const uint32_t *rowCoef;     // Q x taps (c, c) splats
     const int4 *cols;            // per column {work byte offset of the even start, magic, shift, 0}
     const uint32_t *colCoef;     // dstW x NP pairs
     // column split: `parts` workgroups per (band, frame), part k writes output columns
     // [xs[k], xs[k+1]) from source columns [cs[k], ce[k]) (multiples of 4); parts = 1: the whole row
     int parts;                   // 1, 2 or 4
+    int threads;                 // threads per workgroup (4 source columns each): 512 / parts, or 512
+                                 // when the source is wider than 2048 columns (parts of 512 threads)
     int xs[5], cs[4], ce[4];
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
@@ -208,6 +212,8 @@ struct AreaDev {
     int KY, KX, srcW, dstW, dstH;
     uint32_t cy[16];             // (c, c) u16 pairs
     uint32_t cx[8];              // (c_2p, c_2p+1) u16 pairs
+    int lin;                     // 1: Linear at exactly 2:1 (linear_d2_body: taps 2i+1, 2i+2, edge
+    int srcH;                    //    rows / columns replicated); cy[0..1] / cx[0] its two taps
 };
 hipError_t launch_area_int(const AreaDev &a, const Io &io, int rowBegin, int rowEnd, hipStream_t s);
 

@@ -588,6 +588,36 @@ void pick_fast_linear(Plan *p)
     p->kernel = 3;  // IQO_KERNEL_LINEAR_UP2
 }
 
+// Linear at exactly 2:1 (e.g. 3840x2160 -> 1920x1080): main output i blends source samples 2i + 1
+// and 2i + 2 with the table's two taps (IQOLinearResizerImpl_Generic.cpp:210-282, 366-407) and the
+// first / last output replicates the edge sample (:227-237, :329-364), on both axes -- the Area
+// arithmetic (u16 work row, (s + 2^22) >> 23) on odd-aligned pairs: kernels.hip linear_d2_body,
+// dispatched as IQO_KERNEL_AREA_INT (area_kind 8).
+void pick_fast_linear_down(Plan *p)
+{
+    AxisPlan &x = p->x, &y = p->y;
+    if (x.identity || y.identity || x.phases != 1 || y.phases != 1 || x.taps != 2 || y.taps != 2)
+        return;
+    if (p->srcW != 2 * p->dstW || p->srcH != 2 * p->dstH || p->srcW % 16 || p->dstW < 16 || p->dstH < 2)
+        return;
+    for (const AxisPlan *a : {&x, &y}) {
+        const int n = a->dstLen;
+        if (a->coord[0].kind != kBorderLo || a->coord[static_cast<size_t>(n - 1)].kind != kBorderHi)
+            return;
+        for (int i = 1; i < n - 1; ++i) {
+            const CoordInfo &c = a->coord[static_cast<size_t>(i)];
+            if (c.kind != kMain || c.srcO != 2 * i + 1 || c.tabOff != 0)
+                return;
+        }
+    }
+    p->far.KX = 2;
+    p->far.KY = 2;
+    p->far.lin = true;
+    p->far.cx.assign(x.table.begin(), x.table.end());
+    p->far.cy.assign(y.table.begin(), y.table.end());
+    p->kernel = 2;  // IQO_KERNEL_AREA_INT
+}
+
 } // namespace
 
 bool build_tables(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW, size_t dstH,
@@ -659,6 +689,8 @@ bool build_plan(Method m, unsigned degree, size_t srcW, size_t srcH, size_t dstW
         coords_linear(&p->x);
         coords_linear(&p->y);
         pick_fast_linear(p);
+        if (p->kernel == 0)
+            pick_fast_linear_down(p);
         break;
     }
     return true;
@@ -953,35 +985,37 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
 {
     *u = Up2Tables();
     (void)w;
-    if (p.method != kLanczos || p.x.identity || p.y.identity || p.dstW != 2 * p.srcW ||
-        p.dstH != 2 * p.srcH || p.dstW % 16 || p.dstW < 32 || p.dstH < 8)
+    const int F = p.dstW == 2 * p.srcW ? 2 : 3;  // lane: 8 source columns, 8F output columns
+    if (p.method != kLanczos || p.x.identity || p.y.identity || p.dstW != F * p.srcW ||
+        p.dstH != F * p.srcH || p.dstW % (8 * F) || p.dstW < 16 * F || p.dstH < 4 * F)
         return;
     const int NT = static_cast<int>(p.x.taps);
     if ((NT != 4 && NT != 6) || static_cast<int>(p.y.taps) != NT)
         return;
     // every window (main or masked border) starts where the kernel's fixed offset says and takes
-    // its parity's phase table, so the kernel's unmasked sums over zero-padded rows / columns are
-    // the reference's masked numerators
-    auto fixed = [&](const AxisPlan &ax, int i, std::vector<int32_t> (&set)[2]) {
+    // its phase's table, so the kernel's unmasked sums over zero-padded rows / columns are the
+    // reference's masked numerators
+    auto fixed = [&](const AxisPlan &ax, int i, std::vector<int32_t> (&set)[3]) {
         const CoordInfo &ci = ax.coord[static_cast<size_t>(i)];
-        if (ci.kind == kIdentity || ci.srcO != (i >> 1) + 1 - NT / 2 || ci.tabOff % NT != 0)
+        if (ci.kind == kIdentity || ci.srcO != i / F + 1 - NT / 2 || ci.tabOff % NT != 0)
             return false;
         const std::vector<int32_t> c(ax.table.begin() + ci.tabOff, ax.table.begin() + ci.tabOff + NT);
-        std::vector<int32_t> &ref = set[i & 1];
+        std::vector<int32_t> &ref = set[i % F];
         if (ref.empty())
             ref = c;
         return ref == c;
     };
-    std::vector<int32_t> ys[2], xs[2];
+    std::vector<int32_t> ys[3], xs[3];
+    const int EC = 8 * F;  // edge-lane columns
     for (int x = 0; x < p.dstW; ++x) {
         if (!fixed(p.x, x, xs))
             return;
         const Window win = axis_window(p, p.x, x, true);
-        const int side = x < 16 ? 0 : x >= p.dstW - 16 ? 1 : -1;
+        const int side = x < EC ? 0 : x >= p.dstW - EC ? 1 : -1;
         if (win.border && side < 0)
             return;
         if (side >= 0) {
-            const int j = side ? x - (p.dstW - 16) : x;
+            const int j = side ? x - (p.dstW - EC) : x;
             if (!magic_x(win.border ? win.div : (1 << 20), &u->xM[side][j], &u->xT[side][j]))
                 return;
         }
@@ -1004,7 +1038,10 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
         return;
     if (m1 < 0)
         m1 = p.dstH;
-    if (m0 > 8 || p.dstH - m1 > 8 || ys[0].empty() || ys[1].empty() || xs[0].empty() || xs[1].empty())
+    for (int j = 0; j < F; ++j)
+        if (ys[j].empty() || xs[j].empty())
+            return;
+    if (m0 > 16 || p.dstH - m1 > 16)
         return;
     for (int y = 0; y < p.dstH; ++y) {
         if (y >= m0 && y < m1)
@@ -1022,17 +1059,20 @@ void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u)
     };
     if (!single(ys[0]) || !single(xs[0]))
         return;
+    u->F = F;
     u->NT = NT;
     u->m0 = m0;
     u->m1 = m1;
     auto splat = [](int32_t c) { return (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u; };
     u->cy0 = splat(ys[0][static_cast<size_t>(NT / 2 - 1)]);
-    for (int i = 0; i < NT; ++i)
-        u->cy1[i] = splat(ys[1][static_cast<size_t>(i)]);
     u->cx0 = static_cast<uint32_t>(xs[0][static_cast<size_t>(NT / 2 - 1)]) & 0xffffu;
-    for (int q = 0; q < NT / 2; ++q)
-        u->cx1[q] = (static_cast<uint32_t>(xs[1][static_cast<size_t>(2 * q)]) & 0xffffu) |
-                    (static_cast<uint32_t>(xs[1][static_cast<size_t>(2 * q + 1)]) << 16);
+    for (int j = 1; j < F; ++j) {
+        for (int i = 0; i < NT; ++i)
+            u->cy1[j - 1][i] = splat(ys[j][static_cast<size_t>(i)]);
+        for (int q = 0; q < NT / 2; ++q)
+            u->cx1[j - 1][q] = (static_cast<uint32_t>(xs[j][static_cast<size_t>(2 * q)]) & 0xffffu) |
+                               (static_cast<uint32_t>(xs[j][static_cast<size_t>(2 * q + 1)]) << 16);
+    }
     u->ok = true;
 }
 
@@ -1314,48 +1354,70 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
 void build_ryx(const Plan &p, RyxTables *t)
 {
     *t = RyxTables();
-    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 2048 || p.dstW > 1024 || p.srcW % 4 ||
+    // widths: launch_ryx's limits (up to 4 column parts of 512 threads; abi.cpp ryx_dev drops the
+    // kernel when no split fits)
+    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
         p.srcW < 16 || p.dstH < 4)
         return;
     // downscales only (the kernel's register window holds the rows of one group of Q outputs)
     const int64_t g = std::gcd(static_cast<int64_t>(p.srcH), static_cast<int64_t>(p.dstH));
     const int P = static_cast<int>(p.srcH / g), Q = static_cast<int>(p.dstH / g);
     const int T = p.y.taps;
-    const int off = p.method == kLanczos ? 1 - T / 2 : 0;
-    // instantiated (P, Q, taps, method) shapes: kernels.hip launch_ryx
+    if (p.y.phases != Q || P <= Q)
+        return;
+    // Lanczos: outer taps that quantise to zero in every phase are dropped (a zero tap adds
+    // nothing to the sum; a masked border row's divisor is the reference's own, magic_y below):
+    // Lanczos-3 9:4 takes 12 of 14 rows, 4:1 14 of 24, Lanczos-4 2:1 12 of 16
+    int trimLo = 0, trimHi = 0;
+    if (p.method == kLanczos) {
+        trimLo = trimHi = T;
+        for (int j = 0; j < Q; ++j) {
+            const int32_t *c = &p.y.table[static_cast<size_t>(j * T)];
+            int lo = 0, hi = 0;
+            while (lo < T && c[lo] == 0)
+                ++lo;
+            while (hi < T - lo && c[T - 1 - hi] == 0)
+                ++hi;
+            trimLo = std::min(trimLo, lo);
+            trimHi = std::min(trimHi, hi);
+        }
+        if (trimLo + trimHi >= T)
+            return;
+    }
+    const int TE = T - trimLo - trimHi;
+    // instantiated (method, P, Q, taps, column pairs) shapes: kernels.hip launch_ryx.  The fewest
+    // taps >= TE (the window may keep some zero taps), then the fewest pairs that hold every column
+    // window (an odd start takes one more entry)
     struct Shape {
         int method, P, Q, T, NP;
     };
-    static const Shape kShapes[] = {{kLanczos, 9, 4, 14, 8}, {kLanczos, 9, 4, 14, 10}, {kLanczos, 9, 4, 10, 6},
-                                    {kLanczos, 9, 4, 10, 7}, {kArea, 9, 4, 4, 3}};
-    int NP = 0;  // the fewest pairs that hold every column window
+    static const Shape kShapes[] = {{kLanczos, 9, 4, 12, 8},  {kLanczos, 9, 4, 12, 10}, {kLanczos, 9, 4, 8, 6},
+                                    {kLanczos, 9, 4, 8, 7},   {kArea, 9, 4, 4, 3},      {kLanczos, 4, 1, 14, 9},
+                                    {kLanczos, 4, 1, 14, 13}, {kLanczos, 2, 1, 4, 3},   {kLanczos, 2, 1, 12, 9},
+                                    {kLanczos, 2, 1, 16, 11}, {kLanczos, 2, 1, 18, 13}, {kLanczos, 2, 1, 20, 15},
+                                    {kLanczos, 2, 1, 22, 17}, {kLanczos, 2, 1, 24, 19}};
+    const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.P == P && S.Q == Q && S.T == T && p.x.taps + 1 <= 2 * S.NP && !NP)
-            NP = S.NP;
-    // the column windows (an odd start takes one more entry) must fit the instantiation's NP pairs
-    if (!NP || p.y.phases != Q || p.x.taps + 1 > 2 * NP)
+        if (S.method == p.method && S.P == P && S.Q == Q && S.T >= TE && S.T <= T && p.x.taps + 1 <= 2 * S.NP &&
+            (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))
+            best = &S;
+    if (!best)
         return;
-    // rows: every window starts at P m + floor(P j / Q) + off and takes phase j
+    const int TK = best->T, NP = best->NP;
+    const int lo = std::min(trimLo, T - TK);  // the kernel window: taps [lo, lo + TK) of every phase
+    const int off = (p.method == kLanczos ? 1 - T / 2 : 0) + lo;
+    // rows: every reference window starts at P m + floor(P j / Q) + (off - lo) and takes phase j
     for (int y = 0; y < p.dstH; ++y) {
         const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
         const int m = y / Q, j = y % Q;
-        if (ci.kind == kIdentity || ci.srcO != P * m + (P * j) / Q + off || ci.tabOff != j * T)
+        if (ci.kind == kIdentity || ci.srcO != P * m + (P * j) / Q + off - lo || ci.tabOff != j * T)
             return;
     }
-    // Lanczos: the first and last taps of every phase quantise to zero at these ratios (the kernel
-    // windows start one row later and take two taps fewer: 4 of 28 row MACs at Lanczos-3, and a
-    // register window of 18 rows instead of 27); exact, since a zero tap adds nothing to the sum,
-    // and a masked border row's divisor is the reference's own (magic_y below)
-    const int trim = p.method == kLanczos ? 1 : 0;
-    for (int j = 0; j < Q && trim; ++j)
-        if (p.y.table[static_cast<size_t>(j * T)] != 0 || p.y.table[static_cast<size_t>(j * T + T - 1)] != 0)
-            return;
-    const int TE = T - 2 * trim;
-    t->rowCoef.resize(static_cast<size_t>(Q * TE));
+    t->rowCoef.resize(static_cast<size_t>(Q * TK));
     for (int j = 0; j < Q; ++j)
-        for (int k = 0; k < TE; ++k) {
-            const uint32_t c = static_cast<uint32_t>(p.y.table[static_cast<size_t>(j * T + trim + k)]) & 0xffffu;
-            t->rowCoef[static_cast<size_t>(j * TE + k)] = c * 0x10001u;
+        for (int k = 0; k < TK; ++k) {
+            const uint32_t c = static_cast<uint32_t>(p.y.table[static_cast<size_t>(j * T + lo + k)]) & 0xffffu;
+            t->rowCoef[static_cast<size_t>(j * TK + k)] = c * 0x10001u;
         }
     int m0 = 0, m1 = p.dstH;
     if (p.method == kLanczos) {
@@ -1378,7 +1440,7 @@ void build_ryx(const Plan &p, RyxTables *t)
             return;
         if (m1 < 0)
             m1 = p.dstH;
-        if (m0 > 8 || p.dstH - m1 > 8)
+        if (m0 > 16 || p.dstH - m1 > 16)
             return;
         for (int y = 0; y < p.dstH; ++y) {
             if (y >= m0 && y < m1)
@@ -1421,8 +1483,8 @@ void build_ryx(const Plan &p, RyxTables *t)
     }
     t->P = P;
     t->Q = Q;
-    t->taps = TE;
-    t->off = off + trim;
+    t->taps = TK;
+    t->off = off;
     t->NP = NP;
     t->m0 = m0;
     t->m1 = m1;

@@ -85,6 +85,7 @@ bool magic_x(int64_t d, uint32_t *m, int32_t *t);
 struct FastArea {
     int KY = 0, KX = 0;
     std::vector<uint16_t> cy, cx;
+    bool lin = false;  // Linear at exactly 2:1 (taps 2i + 1, 2i + 2, replicated edges): linear_d2_body
 };
 
 struct FastLinear {
@@ -187,21 +188,22 @@ struct WalkTables {
 };
 void build_walk_tables(const Plan &p, const TileTables &t, WalkTables *w);
 
-// Exact 2x Lanczos upscale (kernels.hip lanczos_up2_kernel).  An even output y (x) is the source
-// sample y/2 times one coefficient and an odd one takes NT = 2 * degree taps starting at
-// (y >> 1) + 1 - NT/2, one coefficient set per parity, at the masked borders too.  The kernel takes
-// every row and column: source rows / columns outside the image read as zero, and the border rows
-// (<= 8 per side) and columns (<= 16 per side) are divided in the kernel.
+// Exact 2x and 3x Lanczos upscales (kernels.hip lanczos_up2_kernel).  Output y (x) = F k + j: phase
+// 0 is the source sample k times one coefficient, phases 1 .. F-1 take NT = 2 * degree taps starting
+// at k + 1 - NT/2, one coefficient set per phase, at the masked borders too.  The kernel takes every
+// row and column: source rows / columns outside the image read as zero, and the border rows
+// (<= 16 per side) and columns (<= 8F per side) are divided in the kernel.
 struct Up2Tables {
     bool ok = false;
+    int F = 0;                      // factor (2 or 3): output y = F k + j takes phase j
     int NT = 0;
     int m0 = 0, m1 = 0;             // main rows; the others are masked border rows
-    uint32_t xM[2][16] = {};        // edge lanes (left: columns 0..15, right: dstW - 16 ..):
-    int32_t xT[2][16] = {};         //   floor(s / D) = umulhi(s, xM) >> xT (D = 2^20 off the border)
-    uint32_t yM[2][8] = {};         // border row y (top: y, bottom: y - m1): int16(n * 64 / deno)
-    int32_t yS[2][8] = {};
-    uint32_t cy0 = 0, cy1[6] = {};  // (c, c) u16 splats: even rows' single tap, odd rows' taps
-    uint32_t cx0 = 0, cx1[3] = {};  // (c, 0) / (c_2q, c_2q+1) int16 pairs for even / odd columns
+    uint32_t xM[2][24] = {};        // edge lanes (left: columns 0 .. 8F-1, right: dstW - 8F ..):
+    int32_t xT[2][24] = {};         //   floor(s / D) = umulhi(s, xM) >> xT (D = 2^20 off the border)
+    uint32_t yM[2][16] = {};        // border row y (top: y, bottom: y - m1): int16(n * 64 / deno)
+    int32_t yS[2][16] = {};
+    uint32_t cy0 = 0, cy1[2][6] = {};  // (c, c) u16 splats: phase 0's single tap, phases 1 .. F-1
+    uint32_t cx0 = 0, cx1[2][3] = {};  // (c, 0) / (c_2q, c_2q+1) int16 pairs, same phases
 };
 void build_up2(const Plan &p, const WalkTables &w, Up2Tables *u);
 
@@ -252,17 +254,17 @@ void build_d31(const Plan &p, D31Tables *t);
 // an exact division constant per column (Lanczos border columns; the identity 2^20 elsewhere).
 struct RyxTables {
     bool ok = false;
-    int P = 0, Q = 0, taps = 0, off = 0;   // the instantiation this plan needs (kernels.hip kRyxShapes)
+    int P = 0, Q = 0, taps = 0, off = 0;   // the instantiation this plan needs (kernels.hip launch_ryx)
     int NP = 0;                            // coefficient pairs per column
     int m0 = 0, m1 = 0;                    // Lanczos main rows; the others are masked border rows
-    uint32_t yM[2][8] = {};                // border row y (top: y, bottom: y - m1): magic_y
-    int32_t yS[2][8] = {};
+    uint32_t yM[2][16] = {};               // border row y (top: y, bottom: y - m1): magic_y
+    int32_t yS[2][16] = {};
     std::vector<uint32_t> rowCoef;         // Q x taps (c, c) u16 splats: phase j's taps
     std::vector<int32_t> cols;             // dstW x 4: {work byte offset of the even start, magic, shift, 0}
     std::vector<uint32_t> colCoef;         // dstW x NP coefficient pairs from the even start
 };
 // Work-row padding (u16 entries) left of source column 0 in the kernel's LDS work row.
-constexpr int kRyxPad = 16;
+constexpr int kRyxPad = 24;
 void build_ryx(const Plan &p, RyxTables *t);
 
 // Exact 2:3 Lanczos-3 upscale (kernels.hip lanczos_u23_kernel), e.g. 1280x720 -> 1920x1080.  In the

@@ -37,6 +37,25 @@ SHAPES = [
     # round 3: exact vertical ratio, tabled columns (ryx)
     ("lanczos", 2, 1920, 1080, 854, 480),
     ("lanczos", 3, 1920, 1080, 640, 480),
+    # round 4: the common shapes VERDICT r03 listed on the tile / walk kernels
+    ("linear", 0, 3840, 2160, 1920, 1080),
+    ("lanczos", 3, 3840, 2160, 960, 540),
+    ("lanczos", 4, 3840, 2160, 1920, 1080),
+    ("lanczos", 5, 3840, 2160, 1920, 1080),
+    ("lanczos", 6, 3840, 2160, 1920, 1080),
+    ("lanczos", 7, 3840, 2160, 1920, 1080),
+    ("lanczos", 8, 3840, 2160, 1920, 1080),
+    ("lanczos", 9, 3840, 2160, 1920, 1080),
+    ("lanczos", 4, 1920, 1080, 960, 540),
+    ("lanczos", 2, 3840, 2160, 960, 540),
+    ("lanczos", 1, 3840, 2160, 1920, 1080),
+    ("lanczos", 3, 1280, 720, 3840, 2160),
+    ("linear", 0, 1280, 720, 3840, 2160),
+    ("lanczos", 3, 640, 480, 1920, 1080),
+    ("lanczos", 3, 1920, 1080, 1366, 768),
+    ("area", 0, 1920, 1080, 1366, 768),
+    ("lanczos", 2, 1920, 1080, 1024, 576),
+    ("linear", 0, 1920, 1080, 1280, 720),
 ]
 
 

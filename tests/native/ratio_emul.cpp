@@ -37,7 +37,7 @@ uint8_t edge_div(int s, uint32_t m, int t)
 
 extern "C" {
 
-// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23, 4 = linear_u23, 5 = lanczos_d31, 6 = ryx.  Returns 0 on success, 1 if the shape is
+// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23, 4 = linear_u23, 5 = lanczos_d31, 6 = ryx, 7 = linear_d2.  Returns 0 on success, 1 if the shape is
 // not eligible for that kernel, -1 on bad arguments.
 int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int dstW, int dstH, int pxScale,
                const uint8_t *src, uint8_t *dst)
@@ -94,17 +94,17 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
         build_up2(p, w, &u);
         if (!u.ok)
             return 1;
-        const int NT = u.NT, OFF = 1 - NT / 2;
+        const int NT = u.NT, OFF = 1 - NT / 2, F = u.F, EC = 8 * F;
         for (int y = 0; y < dstH; ++y) {
-            const int k = y >> 1;
+            const int k = y / F, j = y % F;
             for (int c = 0; c < srcW; ++c) {
                 uint16_t acc;
-                if ((y & 1) == 0) {
+                if (j == 0) {
                     acc = static_cast<uint16_t>(px(k, c) * static_cast<uint16_t>(u.cy0));
                 } else {
                     acc = 0;
                     for (int i = 0; i < NT; ++i)
-                        acc = static_cast<uint16_t>(acc + px(k + OFF + i, c) * static_cast<uint16_t>(u.cy1[i]));
+                        acc = static_cast<uint16_t>(acc + px(k + OFF + i, c) * static_cast<uint16_t>(u.cy1[j - 1][i]));
                 }
                 if (y < u.m0 || y >= u.m1) {
                     const int side = y < u.m0 ? 0 : 1, bi = side ? y - u.m1 : y;
@@ -115,16 +115,18 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
             auto W = [&](int c) -> int { return (c < 0 || c >= srcW) ? 0 : static_cast<int16_t>(work[static_cast<size_t>(c)]); };
             for (int x = 0; x < dstW; ++x) {
                 int s = 1 << 19;
-                if ((x & 1) == 0) {
-                    s += W(x >> 1) * static_cast<int16_t>(u.cx0 & 0xffffu);
+                const int kx = x / F, jx = x % F;
+                if (jx == 0) {
+                    s += W(kx) * static_cast<int16_t>(u.cx0 & 0xffffu);
                 } else {
+                    const uint32_t *cx = u.cx1[jx - 1];
                     for (int q = 0; q < NT / 2; ++q)
-                        s += W((x >> 1) + OFF + 2 * q) * static_cast<int16_t>(u.cx1[q] & 0xffffu) +
-                             W((x >> 1) + OFF + 2 * q + 1) * static_cast<int16_t>(u.cx1[q] >> 16);
+                        s += W(kx + OFF + 2 * q) * static_cast<int16_t>(cx[q] & 0xffffu) +
+                             W(kx + OFF + 2 * q + 1) * static_cast<int16_t>(cx[q] >> 16);
                 }
-                const int side = x < 16 ? 0 : x >= dstW - 16 ? 1 : -1;
+                const int side = x < EC ? 0 : x >= dstW - EC ? 1 : -1;
                 dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(
-                    side < 0 ? sat_u8(s >> 20) : edge_div(s, u.xM[side][side ? x - (dstW - 16) : x], u.xT[side][side ? x - (dstW - 16) : x]));
+                    side < 0 ? sat_u8(s >> 20) : edge_div(s, u.xM[side][side ? x - (dstW - EC) : x], u.xT[side][side ? x - (dstW - EC) : x]));
             }
         }
         return 0;
@@ -270,6 +272,37 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
                     o = static_cast<uint8_t>(u > 255 ? 255 : u);
                 }
                 dst[static_cast<size_t>(y) * dstW + x] = o;
+            }
+        }
+        return 0;
+    }
+    if (kind == 7) {
+        // linear_d2_body (Linear 2:1 through IQO_KERNEL_AREA_INT): main rows / columns blend
+        // samples 2i + 1, 2i + 2; edge rows take one source row at 256, edge columns (w + 128) >> 8
+        if (p.kernel != 2 || !p.far.lin)
+            return 1;
+        for (int y = 0; y < dstH; ++y) {
+            int r0 = 2 * y + 1, r1 = 2 * y + 2;
+            uint16_t c0 = p.far.cy[0], c1 = p.far.cy[1];
+            if (y == 0 || y == dstH - 1) {
+                r0 = r1 = y == 0 ? 0 : srcH - 1;
+                c0 = 256;
+                c1 = 0;
+            }
+            for (int c = 0; c < srcW; ++c)
+                work[static_cast<size_t>(c)] = static_cast<uint16_t>(px(r0, c) * c0 + px(r1, c) * c1);
+            for (int x = 0; x < dstW; ++x) {
+                int v;
+                if (x == 0 || x == dstW - 1) {
+                    const uint16_t wv = work[static_cast<size_t>(x == 0 ? 0 : srcW - 1)];
+                    v = static_cast<int16_t>((wv + 128) >> 8);
+                } else {
+                    const uint32_t sum = (1u << 22) + work[static_cast<size_t>(2 * x + 1)] * static_cast<uint32_t>(p.far.cx[0]) +
+                                         work[static_cast<size_t>(2 * x + 2)] * static_cast<uint32_t>(p.far.cx[1]);
+                    v = static_cast<int16_t>(static_cast<int>(sum) >> 23);
+                }
+                const uint16_t u = static_cast<uint16_t>(v);
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(u > 255 ? 255 : u);
             }
         }
         return 0;

@@ -33,10 +33,12 @@ def driver():
     exe = os.path.join(BUILD, "dropin_cpu")
     src = os.path.join(ROOT, "tests", "native", "dropin_cpu.cpp")
     if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(src), os.path.getmtime(libiqo_amd.LIB_PATH)):
-        subprocess.check_call(["g++", "-O2", "-std=c++11", "-I" + os.path.join(ROOT, "include"), "-o", exe, src,
+        tmp = "%s.%d.tmp" % (exe, os.getpid())  # private name + rename: xdist workers may rebuild together
+        subprocess.check_call(["g++", "-O2", "-std=c++11", "-I" + os.path.join(ROOT, "include"), "-o", tmp, src,
                                "-L" + os.path.dirname(libiqo_amd.LIB_PATH), "-liqo_hip",
                                "-Wl,-rpath," + os.path.dirname(libiqo_amd.LIB_PATH), "-Wl,-rpath,/opt/rocm/lib",
                                "-Wl,-rpath-link,/opt/rocm/lib"])
+        os.replace(tmp, exe)
     return exe
 
 

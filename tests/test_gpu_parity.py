@@ -772,6 +772,9 @@ UP2_SHAPES = [
     ("lanczos", 3, 640, 360, 1280, 720, 1),
     ("lanczos", 3, 392, 100, 784, 200, 1),       # one wave holding both edges
     ("lanczos", 2, 200, 60, 400, 120, 1),
+    ("lanczos", 3, 1280, 720, 3840, 2160, 1),    # 3x: 24 output columns per lane, 3 rows per source row
+    ("lanczos", 2, 640, 360, 1920, 1080, 1),
+    ("lanczos", 3, 136, 40, 408, 120, 1),        # 3x, one wave holding both edges
 ]
 
 
@@ -795,7 +798,7 @@ def test_lanczos_up2_matches_oracle(cfg):
         assert bad.size == 0, (cfg, f, bad[:4].tolist())
     w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
     w.set_option("up2", 0)
-    assert w.describe()["kernel"] == "walk"
+    assert w.describe()["kernel"] in ("walk", "tile")
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
     for opt, val in (("bands", 1), ("bands", 3), ("bands", 7), ("lanes", 5), ("lanes", 62)):
         for alt in (1, 0):  # odd bands walking bottom-up (default) / every band top-down
@@ -1184,6 +1187,15 @@ RYX_SHAPES = [
     ("lanczos", 3, 1920, 1080, 853, 480, 1),     # odd output width: the last column's 1-byte store
     ("area", 0, 1920, 1080, 853, 480, 1),
     ("lanczos", 2, 1280, 720, 569, 320, 1),
+    ("lanczos", 3, 3840, 2160, 960, 540, 1),     # 4:1 (14 of 24 row taps, 13 pairs), two 512-thread parts
+    ("lanczos", 2, 1920, 1080, 480, 270, 1),     # 4:1 (14 of 16 row taps)
+    ("lanczos", 1, 1280, 720, 640, 360, 1),      # 2:1 Lanczos-1
+    ("lanczos", 4, 1920, 1080, 960, 540, 1),     # 2:1 Lanczos-4 .. -9: 12 .. 24 row taps
+    ("lanczos", 5, 1280, 720, 640, 360, 1),
+    ("lanczos", 6, 1280, 720, 639, 360, 1),
+    ("lanczos", 7, 720, 480, 360, 240, 1),
+    ("lanczos", 8, 1280, 720, 640, 360, 1),
+    ("lanczos", 9, 3840, 2160, 1920, 1080, 1),
 ]
 
 
@@ -1207,7 +1219,7 @@ def test_ryx_matches_oracle(cfg):
         assert bad.size == 0, (cfg, f, bad[:4].tolist())
     w = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
     w.set_option("ryx", 0)
-    assert w.describe()["kernel"] in ("walk", "tile")
+    assert w.describe()["kernel"] in ("walk", "tile", "general")
     assert (w.resize_tensor(src).cpu().numpy() == out).all()
     for val in (1, 3, 7, dh):
         b = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
@@ -1249,6 +1261,73 @@ def test_ryx_matches_oracle(cfg):
     torch.cuda.synchronize()
     ob = obuf.cpu().numpy()
     assert ob[0] == 5 and (ob[1:].reshape(n, dh, dw) == out).all(), (cfg, "odd base")
+
+
+LIN2_SHAPES = [
+    (3840, 2160, 1920, 1080),   # Linear 4K -> 1080p
+    (1920, 1080, 960, 540),
+    (640, 480, 320, 240),
+    (48, 6, 24, 3),             # two thread groups per row, three rows (both edge rows)
+    (32, 4, 16, 2),
+]
+
+
+@pytest.mark.parametrize("cfg", LIN2_SHAPES, ids=lambda c: "%dx%d_%dx%d" % c)
+def test_linear_d2_matches_oracle(cfg):
+    """Linear at exactly 2:1 (linear_d2_body through IQO_KERNEL_AREA_INT: taps 2i+1, 2i+2, edge
+    rows and columns replicated): equal to the oracle on noise, flat and half-flat frames, in row
+    bands through their source windows, with padded strides, and through the host-pointer path;
+    the I420 plan runs it for all three planes in one launch."""
+    sw, sh, dw, dh = cfg
+    n = 3
+    frames = _noise_batch(n, sw, sh, 2200)
+    frames[1] = 201
+    frames[2, :, sw // 3:] = 255
+    exp = [ol.run_oracle("linear", 0, sw, sh, dw, dh, 1, frames[f]) for f in range(n)]
+    r = libiqo_amd.make_resizer("linear", 0, sw, sh, dw, dh, 1)
+    assert r.describe()["kernel"] == "area_int"
+    assert libiqo_amd.host_kernel_for("linear", 0, sw, sh, dw, dh, 1) == "area_int"
+    src = torch.from_numpy(frames).to(DEV)
+    out = r.resize_tensor(src).cpu().numpy()
+    for f in range(n):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, f, bad[:4].tolist())
+    got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
+    cuts = sorted(set([0, 1, dh // 3, dh // 2, max(dh - 1, 1), dh]))
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        s0, sn = r.band_src_rows(r0, r1 - r0)
+        win = src[:, s0:s0 + sn].contiguous()
+        r.resize_band(n, r0, r1 - r0, s0, sw, sn * sw, win.data_ptr(), dw, dh * dw, got[:, r0].data_ptr())
+    torch.cuda.synchronize()
+    assert (got.cpu().numpy() == out).all(), cfg
+    sst, dst_st = sw + 32, dw + 8
+    pbuf = torch.zeros((n, sh, sst), dtype=torch.uint8, device=DEV)
+    pbuf[:, :, :sw] = src
+    dbuf = torch.full((n, dh, dst_st), 9, dtype=torch.uint8, device=DEV)
+    r.resize_device(n, sst, sh * sst, pbuf.data_ptr(), dst_st, dh * dst_st, dbuf.data_ptr())
+    torch.cuda.synchronize()
+    assert (dbuf[:, :, :dw].cpu().numpy() == out).all(), cfg
+    assert (dbuf[:, :, dw:].cpu().numpy() == 9).all(), (cfg, "wrote past the row")
+    hout = np.zeros((dh, dw), np.uint8)
+    r.resize(sw, np.ascontiguousarray(frames[0]), dw, hout)
+    assert (hout == exp[0]).all(), (cfg, "host path")
+    if sw % 64 == 0 and sw >= 128 and sh % 4 == 0:  # I420: Y and both chroma planes 2:1, one fused launch
+        yuv = libiqo_amd.Yuv420Resizer("linear", 0, sw, sh, dw, dh)
+        cw, ch = sw // 2, sh // 2
+        chroma = [np.ascontiguousarray(frames[f, :ch, :cw]) for f in range(2)]
+        packed = np.stack([np.concatenate([frames[f].ravel(), chroma[f].ravel(), chroma[f][::-1].ravel()])
+                           for f in range(2)])
+        res, fused = yuv.resize_frames(torch.from_numpy(packed).to(DEV))
+        torch.cuda.synchronize()
+        assert fused == 1
+        res = res.cpu().numpy()
+        cdw, cdh = dw // 2, dh // 2
+        for f in range(2):
+            assert (res[f, :dw * dh].reshape(dh, dw) == exp[f]).all()
+            for p, plane in ((0, chroma[f]), (1, np.ascontiguousarray(chroma[f][::-1]))):
+                ce = ol.run_oracle("linear", 0, cw, ch, cdw, cdh, 1, plane)
+                o0 = dw * dh + p * cdw * cdh
+                assert (res[f, o0:o0 + cdw * cdh].reshape(cdh, cdw) == ce).all(), (cfg, f, p)
 
 
 STACK_SHAPES = [

@@ -17,7 +17,8 @@ import oracle_lib as ol
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
-KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6}
+KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6,
+         "linear_d2": 7}
 
 
 @pytest.fixture(scope="module")
@@ -27,8 +28,11 @@ def emul():
     so = os.path.join(out, "libratio_emul.so")
     srcs = [os.path.join(HERE, "native", "ratio_emul.cpp"), os.path.join(ROOT, "libiqo_amd", "csrc", "plan.cpp")]
     if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
+        # build under a private name and rename: pytest-xdist workers may rebuild at the same time
+        tmp = "%s.%d.tmp" % (so, os.getpid())
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off",
-                               "-I" + os.path.join(ROOT, "libiqo_amd", "csrc"), "-o", so] + srcs)
+                               "-I" + os.path.join(ROOT, "libiqo_amd", "csrc"), "-o", tmp] + srcs)
+        os.replace(tmp, so)
     lib = ctypes.CDLL(so)
     lib.ratio_emul.restype = ctypes.c_int
     lib.ratio_emul.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint] + [ctypes.c_int] * 5 + [ctypes.c_void_p] * 2
@@ -72,7 +76,16 @@ def _shapes():
            ("ryx", "lanczos", 3, 1920, 1080, 854, 480), ("ryx", "lanczos", 2, 1920, 1080, 854, 480),
            ("ryx", "area", 0, 1920, 1080, 854, 480), ("ryx", "lanczos", 3, 1920, 1080, 640, 480),
            ("ryx", "lanczos", 3, 1280, 720, 570, 320), ("ryx", "area", 0, 720, 576, 360, 256),
-           ("ryx", "lanczos", 3, 1920, 1080, 853, 480), ("ryx", "area", 0, 1920, 1080, 853, 480)]  # odd widths
+           ("ryx", "lanczos", 3, 1920, 1080, 853, 480), ("ryx", "area", 0, 1920, 1080, 853, 480),  # odd widths
+           ("linear_d2", "linear", 0, 3840, 2160, 1920, 1080), ("linear_d2", "linear", 0, 640, 480, 320, 240),
+           ("linear_d2", "linear", 0, 32, 4, 16, 2), ("linear_d2", "linear", 0, 48, 6, 24, 3),
+           ("lanczos_up2", "lanczos", 3, 1280, 720, 3840, 2160), ("lanczos_up2", "lanczos", 2, 640, 360, 1920, 1080),  # 3x
+           ("lanczos_up2", "lanczos", 3, 16, 4, 48, 12), ("lanczos_up2", "lanczos", 2, 16, 5, 48, 15),
+           ("ryx", "lanczos", 3, 3840, 2160, 960, 540), ("ryx", "lanczos", 2, 1920, 1080, 480, 270),  # 4:1
+           ("ryx", "lanczos", 1, 640, 480, 320, 240), ("ryx", "lanczos", 4, 1920, 1080, 960, 540),   # 2:1
+           ("ryx", "lanczos", 5, 640, 360, 320, 180), ("ryx", "lanczos", 6, 640, 360, 320, 180),
+           ("ryx", "lanczos", 7, 720, 480, 360, 240), ("ryx", "lanczos", 8, 640, 360, 320, 180),
+           ("ryx", "lanczos", 9, 3840, 2160, 1920, 1080), ("ryx", "lanczos", 9, 5120, 64, 2560, 32)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -81,10 +94,14 @@ def _shapes():
         out.append(("linear_u23", "linear", 0, 8 * a, 2 * b, 12 * a, 3 * b))
         out.append(("area_d32", "area", 0, 12 * a, 3 * b, 8 * a, 2 * b))
         out.append(("lanczos_up2", "lanczos", rng.choice((2, 3)), 8 * a, b + 4, 16 * a, 2 * b + 8))
+        out.append(("lanczos_up2", "lanczos", rng.choice((2, 3)), 8 * a, b + 4, 24 * a, 3 * b + 12))
         out.append(("lanczos_d31", "lanczos", rng.choice((2, 3)), 12 * a + 48, 3 * b + 24, 4 * a + 16, b + 8))
         sw = 4 * rng.randint(20, 500)
+        out.append(("linear_d2", "linear", 0, 16 * a, 2 * b, 8 * a, b))
         out.append(("ryx", rng.choice(("lanczos", "area")), 3, sw, 9 * b + 36,
                     2 * rng.randint(sw // 4 + 1, min(1024, sw) // 2) - rng.randint(0, 1), 4 * b + 16))
+        out.append(("ryx", "lanczos", rng.choice((1, 4, 5, 6, 7, 8, 9)), sw, 2 * b + 40, sw // 2, b + 20))
+        out.append(("ryx", "lanczos", rng.choice((2, 3)), 4 * sw, 4 * b + 40, sw, b + 10))
     return out
 
 

@@ -24,8 +24,10 @@ def emul():
     so = os.path.join(out, "libtile_emul.so")
     srcs = [os.path.join(HERE, "native", "tile_emul.cpp"), os.path.join(ROOT, "libiqo_amd", "csrc", "plan.cpp")]
     if not os.path.exists(so) or any(os.path.getmtime(s) > os.path.getmtime(so) for s in srcs):
+        tmp = "%s.%d.tmp" % (so, os.getpid())  # private name + rename: xdist workers may rebuild together
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-ffp-contract=off",
-                               "-I" + os.path.join(ROOT, "libiqo_amd", "csrc"), "-o", so] + srcs)
+                               "-I" + os.path.join(ROOT, "libiqo_amd", "csrc"), "-o", tmp] + srcs)
+        os.replace(tmp, so)
     lib = ctypes.CDLL(so)
     lib.tile_emul.restype = ctypes.c_int
     lib.tile_emul.argtypes = [ctypes.c_int, ctypes.c_uint] + [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_void_p,
