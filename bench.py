@@ -57,6 +57,13 @@ CONFIGS = {
     # narrow frames (frame-stacked streamer): the C1 I420 chroma plane size, single channel
     "n1": ("lanczos", 2, 320, 240, 160, 120, 1, 16384, "N1 Lanczos-2 U8 1ch 320x240->160x120"),
     "n2": ("lanczos", 3, 640, 360, 320, 180, 1, 4096, "N2 Lanczos-3 U8 1ch 640x360->320x180"),
+    # round 4 kernels: Linear 2:1 (linear_d2), 4:1 and Lanczos-4..9 2:1 (ryx), exact 3x upscales
+    "h1": ("linear", 0, 3840, 2160, 1920, 1080, 1, 128, "H1 Linear U8 1ch 3840x2160->1920x1080"),
+    "h2": ("lanczos", 3, 3840, 2160, 960, 540, 1, 128, "H2 Lanczos-3 U8 1ch 3840x2160->960x540"),
+    "h3": ("lanczos", 4, 3840, 2160, 1920, 1080, 1, 128, "H3 Lanczos-4 U8 1ch 3840x2160->1920x1080"),
+    "h4": ("lanczos", 3, 1280, 720, 3840, 2160, 1, 64, "H4 Lanczos-3 U8 1ch 1280x720->3840x2160"),
+    "h5": ("linear", 0, 1280, 720, 3840, 2160, 1, 64, "H5 Linear U8 1ch 1280x720->3840x2160"),
+    "h6": ("lanczos", 6, 3840, 2160, 1920, 1080, 1, 128, "H6 Lanczos-6 U8 1ch 3840x2160->1920x1080"),
 }
 
 

@@ -772,7 +772,8 @@ iqo_amd::LinearDev linear_dev(const iqo_hip_plan *h)
     l.srcH = p.srcH;
     l.dstW = p.dstW;
     l.dstH = p.dstH;
-    for (int q = 0; q < 2; ++q) {
+    l.F = p.fln.F;
+    for (int q = 0; q < 3; ++q) {
         l.cx[q] = pair16(p.fln.cx[q][0], p.fln.cx[q][1]);
         l.cy[q] = pair16(p.fln.cy[q][0], p.fln.cy[q][1]);
     }

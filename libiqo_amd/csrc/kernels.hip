@@ -73,6 +73,25 @@ __device__ __forceinline__ int sdot2(uint32_t a, uint32_t c, int acc)
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, c), acc, false);
 }
 
+// v_dot2_i32_i16 (VOP3P) with a uniform coefficient pair and the accumulator in a VGPR that stays
+// live: the first dot of an output that starts from the rounding bias.  (The builtin is always
+// selected as v_dot2c, which needs the accumulator in its destination: a v_mov of the bias per
+// output, 72 per source row in the 3x kernel.)
+__device__ __forceinline__ int sdot2_sv(uint32_t a, uint32_t c, int acc)
+{
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(c), "v"(acc));
+    return r;
+}
+
+// (and with per-lane coefficients)
+__device__ __forceinline__ int sdot2_vv(uint32_t a, uint32_t c, int acc)
+{
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(c), "v"(acc));
+    return r;
+}
+
 __device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t c, uint32_t acc)
 {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, c), acc, false);
@@ -125,6 +144,38 @@ __device__ __forceinline__ uint32_t opaque(uint32_t v)
 {
     asm volatile("" : "+v"(v));
     return v;
+}
+
+// One wave's output row of 24-byte lane pieces (the 3x streamers: lanes 1 .. np own output bytes
+// [24 (l - 1), 24 l) of the wave's span, nb = 24 np bytes from byte offset `base`) stored as
+// contiguous 16-byte pieces: staged through the wave's 2 KB of LDS, then lane l stores pieces l and
+// 64 + l.  Two dwordx4 stores at 24-byte strides split most pieces over two 64-byte segments and
+// left both 3x streamers at a third of the 2x ones' bandwidth.  Wave-local LDS operations run in
+// order, so no barrier separates one row's reads from the next row's writes.
+template <int AUX>
+__device__ __forceinline__ void store_row24(uint8_t *sb, const uint32_t (&o)[6], bool produce, int lane, int nb,
+                                            __amdgpu_buffer_rsrc_t dstR, int base)
+{
+    constexpr int OOB = 0x7ff00000;
+    if (produce) {
+        u32x2 *p = reinterpret_cast<u32x2 *>(sb + 24 * (lane - 1));
+        p[0] = u32x2{o[0], o[1]};
+        p[1] = u32x2{o[2], o[3]};
+        p[2] = u32x2{o[4], o[5]};
+    }
+    __builtin_amdgcn_wave_barrier();
+    const u32x4 c0 = *reinterpret_cast<const u32x4 *>(sb + 16 * lane);
+    const u32x4 c1 = *reinterpret_cast<const u32x4 *>(sb + 1024 + 16 * lane);
+    const bool row = base < OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(c0, dstR, row && 16 * lane + 16 <= nb ? base + 16 * lane : OOB, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(c1, dstR, row && 1040 + 16 * lane <= nb ? base + 1024 + 16 * lane : OOB, 0,
+                                           AUX);
+    if (nb & 8) {  // odd np (uniform): the span's last 8 bytes are half a piece
+        const int c = (nb - 8) >> 4;
+        const u32x4 h = c < 64 ? c0 : c1;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{h.x, h.y}, dstR, row && lane == (c & 63) ? base + nb - 8 : OOB, 0,
+                                              AUX);
+    }
 }
 
 // Compile-time loop: f(std::integral_constant<int, 0>) ... f(integral_constant<int, N-1>), so
@@ -2271,7 +2322,11 @@ __global__ __launch_bounds__(256) void linear_d2_kernel(AreaArgs a)
 }
 
 
-// ================================================================ exact 2x bilinear streamer
+// ================================================================ exact 2x / 3x bilinear streamer
+//
+// (3x, F = 3: the same walk; lane l's 24 output columns [3cb, 3cb + 24) read the same work columns
+// [cb - 1, cb + 8], output 3cb + j blends columns cb + floor((j - 1) / 3) and the next with phase
+// j % 3; a source step yields output rows 3k + 1 .. 3k + 3; 16 + 8-byte stores.)
 //
 // One WAVE = one row band of one frame x one strip of source columns, walking the band top to
 // bottom so every source row is fetched from HBM once per band (2x upsampling reads each source
@@ -2315,10 +2370,12 @@ __device__ __forceinline__ uint32_t pack23_hi(uint32_t w, uint32_t a, uint32_t b
     return w;
 }
 
-template <int PD, bool NTST>
+template <int PD, bool NTST, int F>
 __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, const unsigned bx, const unsigned by)
 {
     static_assert(PD % 2 == 0, "the unroll must also cover the 2-slot row ring");
+    constexpr int OPL = 8 * F;  // output columns per lane
+    __shared__ __attribute__((aligned(16))) uint8_t stage[F == 3 ? 4 * 2048 : 16];  // 3x: store_row24
     const LinearDev &g = a.g;
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
@@ -2335,11 +2392,11 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
     const int cb = x0 - 8 + 8 * lane;
     const bool produce = lane >= 1 && lane <= np;
     const int voff = (lane <= np + 1 && cb >= 0 && cb < g.srcW) ? cb : 0x7ff00000;
-    const int stoff = produce ? 2 * cb : 0x7ff00000;
+    const int stoff = produce ? F * cb : 0x7ff00000;
     // replicated border columns (work + 128) >> 8 == (work * 2^15 + 2^22) >> 23: the border lanes
     // take the weight pair (0, 2^15) / (2^15, 0) for their outer output, so no branch is needed
     const uint32_t cxFirst = cb == 0 ? 0x80000000u : g.cx[0];
-    const uint32_t cxLast = cb + 8 == g.srcW ? 0x00008000u : g.cx[1];
+    const uint32_t cxLast = cb + 8 == g.srcW ? 0x00008000u : g.cx[(OPL - 1) % F];
 
     const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(by) * a.io.srcFrameSt;
     uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(by) * a.io.dstFrameSt;
@@ -2349,11 +2406,12 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
 
-    // interior output rows of the band: [max(y0, 1), yl); pair index k covers rows 2k+1, 2k+2
+    // interior output rows of the band: [max(y0, 1), yl); step k covers rows F k + 1 .. F k + F
     const int yl = min(y1, g.dstH - 1);
-    const int kLo = y0 <= 1 ? 0 : (y0 - 1) >> 1;
-    const int kHi = yl >> 1;  // exclusive
-    const int rLast = kHi;    // last source row the loop reads
+    const int kLo = y0 <= 1 ? 0 : (y0 - 1) / F;
+    const int kHi = (yl + F - 2) / F;          // exclusive
+    const int rLast = min(kHi, g.srcH - 1);    // last source row the loop reads (3x: the last main
+                                               // row's second sample has weight 0)
 
     auto load_row = [&](int r) -> u32x2 {
         return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff, r <= rLast ? (r - srcRow0) * srcSt : 0x7ff00000,
@@ -2376,20 +2434,24 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             E[q] = __builtin_amdgcn_alignbit(W[q + 1], W[q], 16);
-        uint32_t s[16];
+        // output F cb + j blends work columns m, m + 1, m = cb + floor((j - 1) / F), phase j % F
+        uint32_t s[OPL];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int r = (j - 1) >> 1;
-            const uint32_t pr = j == 0 ? W[0] : ((r & 1) ? W[(r + 1) >> 1] : E[r >> 1]);
-            s[j] = udot2(pr, j == 0 ? cxFirst : (j == 15 ? cxLast : g.cx[j & 1]), 1u << 22);
+        for (int j = 0; j < OPL; ++j) {
+            const int r = j == 0 ? -1 : (j - 1) / F;
+            const uint32_t pr = r < 0 ? W[0] : ((r & 1) ? W[(r + 1) >> 1] : E[r >> 1]);
+            s[j] = udot2(pr, j == 0 ? cxFirst : (j == OPL - 1 ? cxLast : g.cx[j % F]), 1u << 22);
         }
-        u32x4 o;
-        o.x = pack23_hi(pack23_lo(s[0], s[1]), s[2], s[3]);
-        o.y = pack23_hi(pack23_lo(s[4], s[5]), s[6], s[7]);
-        o.z = pack23_hi(pack23_lo(s[8], s[9]), s[10], s[11]);
-        o.w = pack23_hi(pack23_lo(s[12], s[13]), s[14], s[15]);
-        __builtin_amdgcn_raw_buffer_store_b128(o, dstR, stoff, valid ? (y - dstRow0) * dstSt : 0x7ff00000,
-                                               NTST ? 2 : 0);
+        uint32_t o[OPL / 4];
+#pragma unroll
+        for (int q = 0; q < OPL / 4; ++q)
+            o[q] = pack23_hi(pack23_lo(s[4 * q], s[4 * q + 1]), s[4 * q + 2], s[4 * q + 3]);
+        const int rowOff = valid ? (y - dstRow0) * dstSt : 0x7ff00000;
+        if constexpr (F == 3)
+            store_row24<NTST ? 2 : 0>(stage + 2048 * wib, o, produce, lane, 24 * np, dstR,
+                                      valid ? 3 * x0 + rowOff : 0x7ff00000);
+        else
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{o[0], o[1], o[2], o[3]}, dstR, stoff, rowOff, NTST ? 2 : 0);
     };
     auto border_row = [&](int y, int r) {
         uint32_t P[5];
@@ -2403,8 +2465,13 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
     if (y0 == 0)
         border_row(0, 0);
 
-    const uint32_t c0a = (g.cy[1] & 0xffffu) * 0x10001u, c1a = (g.cy[1] >> 16) * 0x10001u;  // row 2k+1
-    const uint32_t c0b = (g.cy[0] & 0xffffu) * 0x10001u, c1b = (g.cy[0] >> 16) * 0x10001u;  // row 2k+2
+    // row F k + i (i = 1 .. F): phase i % F's (c0, c1) splats
+    uint32_t c0[F], c1[F];
+#pragma unroll
+    for (int i = 1; i <= F; ++i) {
+        c0[i - 1] = (g.cy[i % F] & 0xffffu) * 0x10001u;
+        c1[i - 1] = (g.cy[i % F] >> 16) * 0x10001u;
+    }
     uint32_t U[2][5];
     u32x2 pre[PD];
     unpack(load_row(kLo), U[0]);
@@ -2415,8 +2482,9 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
     for (int i = 0; i < PD; ++i) {
         __builtin_amdgcn_sched_barrier(0);
         pre[i] = load_row(kLo + 1 + i);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, 0x7ff00000, 0x7ff00000 + 32 * i, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, 0x7ff00000, 0x7ff00010 + 32 * i, 0);
+#pragma unroll
+        for (int j = 0; j < 2 * F - 2; ++j)  // (2x: one store per row, 3x: two)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, dstR, 0x7ff00000, 0x7ff00000 + 64 * (F * i + j), 0);
     }
     for (int base = kLo; base < kHi; base += PD) {
         static_for<PD>([&](auto uc) {
@@ -2431,29 +2499,33 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
             pre[v] = load_row(k + 1 + PD);
             const uint32_t(&A)[5] = U[v % 2];
             const uint32_t(&B)[5] = U[(v + 1) % 2];
-            uint32_t W[5];
 #pragma unroll
-            for (int q = 0; q < 5; ++q)
-                W[q] = pk_mad(B[q], c1a, pk_mul(A[q], c0a));
-            emit(W, 2 * k + 1, 2 * k + 1 >= y0 && 2 * k + 1 < yl);
+            for (int i = 1; i <= F; ++i) {
+                uint32_t W[5];
 #pragma unroll
-            for (int q = 0; q < 5; ++q)
-                W[q] = pk_mad(B[q], c1b, pk_mul(A[q], c0b));
-            emit(W, 2 * k + 2, 2 * k + 2 >= y0 && 2 * k + 2 < yl);
+                for (int q = 0; q < 5; ++q)
+                    W[q] = pk_mad(B[q], c1[i - 1], pk_mul(A[q], c0[i - 1]));
+                const int y = F * k + i;
+                emit(W, y, y >= y0 && y < yl);
+            }
         });
     }
 
     if (y1 == g.dstH && g.dstH > 1)
         border_row(g.dstH - 1, g.srcH - 1);
 }
-template <int PD, bool NTST>
+template <int PD, bool NTST, int F>
 __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 {
-    linear_up2_kernel_body<PD, NTST>(a, blockIdx.x, blockIdx.y);
+    linear_up2_kernel_body<PD, NTST, F>(a, blockIdx.x, blockIdx.y);
 }
 
 
-// ================================================================ exact 2x Lanczos upscale
+// ================================================================ exact 2x / 3x Lanczos upscale
+//
+// (3x, F = 3: output F k + j takes phase j; phase 0 is the single tap, phases 1 and 2 both take NT
+// taps from k + 1 - NT/2.  A lane owns the same 8 source columns and 24 output columns, a source
+// step yields F output rows, and the edge lanes park 24 sums per row.  1280x720 -> 3840x2160.)
 //
 // Lanczos-2/3 at exactly 2x (plan.cpp build_up2).  In the reference's tables for this ratio an
 // even output row / column sits exactly on a source sample (a single tap: 64 vertically, 2^14
@@ -2496,7 +2568,10 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     constexpr int OPL = 8 * F;       // output columns per lane
     constexpr int OOB = 0x7ff00000;
     const Up2Dev &u = a.u;
+    // the rounding bias in a VGPR, the first dot's third operand (sdot2_sv)
+    const int bias = static_cast<int>(opaque(1u << 19));
     __shared__ int4 park[4][2][F * NW][OPL / 4];  // per wave, side, row slot: the edge lane's raw sums
+    __shared__ __attribute__((aligned(16))) uint8_t stage[F == 3 ? 4 * 2048 : 16];  // 3x: store_row24
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
@@ -2603,12 +2678,12 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
             const int m = j / F, ph = j % F;  // output F (cb + m) + ph
             if (ph == 0) {
                 // on a source column: c * w[cb + m] (the pair's high half meets a zero coefficient)
-                sum[j] = sdot2(pair(m + 4), u.cx0, 1 << 19);
+                sum[j] = sdot2_sv(pair(m + 4), u.cx0, bias);
             } else {
                 const int rel = m + OFF + 4;
-                int acc = 1 << 19;
+                int acc = sdot2_sv(pair(rel), u.cx1[ph - 1][0], bias);
 #pragma unroll
-                for (int q = 0; q < H; ++q)
+                for (int q = 1; q < H; ++q)
                     acc = sdot2(pair(rel + 2 * q), u.cx1[ph - 1][q], acc);
                 sum[j] = acc;
             }
@@ -2617,7 +2692,11 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
 #pragma unroll
         for (int q = 0; q < OPL / 4; ++q)
             o[q] = pack_hi(pack_lo(sum[4 * q], sum[4 * q + 1]), sum[4 * q + 2], sum[4 * q + 3]);
-        store_row(o, stoff, y, y >= y0 && y < y1);
+        if constexpr (F == 3)
+            store_row24<2>(stage + 2048 * wib, o, produce, lane, 24 * a.np, dstR,
+                           y >= y0 && y < y1 ? x0 + (y - dstRow0) * dstSt : OOB);
+        else
+            store_row(o, stoff, y, y >= y0 && y < y1);
         if (edgeL || edgeR) {  // uniform
             if (laneL || laneR) {
                 int4 *pk = park[wib][laneL ? 0 : 1][slot];
@@ -2847,7 +2926,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         for (int j = 0; j < 8; ++j) {
             const int ph = j & 1;
             const int rel = 3 * (j >> 1) + BX0 + ph;  // window start of output x0 + 8(l-1) + j
-            int acc = sdot2(pair(rel), d.cx[ph][0], 1 << 19);
+            int acc = sdot2_sv(pair(rel), d.cx[ph][0], 1 << 19);
 #pragma unroll
             for (int q = 1; q < NPX; ++q)
                 acc = sdot2(pair(rel + 2 * q), d.cx[ph][q], acc);
@@ -3113,9 +3192,9 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
             const int st = S::XS + 3 * j;           // window start (tap 0) relative to cb
             const bool odd = (st & 1) != 0;
             const int e0 = ((odd ? st + 1 : st) - S::EB) / 2;
-            int acc = 1 << 19;
+            int acc = sdot2_sv(E[e0], odd ? d.cxo[0] : d.cxe[0], 1 << 19);
 #pragma unroll
-            for (int q = 0; q < S::NPX; ++q)
+            for (int q = 1; q < S::NPX; ++q)
                 acc = sdot2(E[e0 + q], odd ? d.cxo[q] : d.cxe[q], acc);
             sum[j] = acc;
         }
@@ -3447,9 +3526,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
                 int acc[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
-                    acc[k] = 1 << 19;
+                    acc[k] = sdot2_vv(w[k][0], cf[k][0], 1 << 19);
 #pragma unroll
-                    for (int q = 0; q < NP; ++q)
+                    for (int q = 1; q < NP; ++q)
                         acc[k] = sdot2(w[k][q], cf[k][q], acc[k]);
                 }
                 if (edgeT) {
@@ -3594,10 +3673,10 @@ __global__ __launch_bounds__(256) void lanczos_u23_kernel(U23Args a)
         for (int j = 0; j < 12; ++j) {
             const int g = j / 3, ph = j % 3;
             if (ph == 0) {
-                sum[j] = sdot2(pair(2 * g), d.cx0, 1 << 19);
+                sum[j] = sdot2_sv(pair(2 * g), d.cx0, 1 << 19);
             } else {
                 const int rel = 2 * g - 2 + (ph - 1);
-                int acc = sdot2(pair(rel), d.cx[ph - 1][0], 1 << 19);
+                int acc = sdot2_sv(pair(rel), d.cx[ph - 1][0], 1 << 19);
 #pragma unroll
                 for (int q = 1; q < 3; ++q)
                     acc = sdot2(pair(rel + 2 * q), d.cx[ph - 1][q], acc);
@@ -4014,7 +4093,7 @@ struct LinearD2Plane {
 struct LinearPlane {
     static __device__ __forceinline__ void run(const LinearArgs &a, unsigned bx, unsigned by)
     {
-        linear_up2_kernel_body<2, true>(a, bx, by);
+        linear_up2_kernel_body<2, true, 2>(a, bx, by);
     }
 };
 
@@ -4380,21 +4459,24 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         return hipErrorInvalidValue;
     // instantiations (plan.cpp build_ryx kShapes): method, P, Q, taps (the reference's taps less the
     // zero outer taps of every phase), column pairs
+    // PD: groups of P source rows loaded ahead (ubench: with one group in flight the source loads
+    // cost G5 19 % and Lanczos-4 2:1 27 % of the kernel time -- latency, not bandwidth)
     struct Inst {
         bool lz;
         int P, Q, T, NP;
         const void *kern;
     };
-#define IQO_RYX(LZ_, P_, Q_, T_, NP_) {LZ_, P_, Q_, T_, NP_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, 1>)}
+#define IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_)                                                                      \
+    {LZ_, P_, Q_, T_, NP_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_>)}
     static const Inst kInst[] = {
-        IQO_RYX(true, 9, 4, 12, 8), IQO_RYX(true, 9, 4, 12, 10),   // Lanczos-3 9:4 (1080p -> 480p, -> 640x480)
-        IQO_RYX(true, 9, 4, 8, 6), IQO_RYX(true, 9, 4, 8, 7),      // Lanczos-2 9:4
-        IQO_RYX(false, 9, 4, 4, 3),                                // Area 9:4
-        IQO_RYX(true, 4, 1, 14, 13), IQO_RYX(true, 4, 1, 14, 9),   // Lanczos-3 / -2 4:1 (4K -> 960x540)
-        IQO_RYX(true, 2, 1, 4, 3),                                 // Lanczos-1 2:1
-        IQO_RYX(true, 2, 1, 12, 9), IQO_RYX(true, 2, 1, 16, 11),   // Lanczos-4 / -5 2:1
-        IQO_RYX(true, 2, 1, 18, 13), IQO_RYX(true, 2, 1, 20, 15),  // Lanczos-6 / -7 2:1
-        IQO_RYX(true, 2, 1, 22, 17), IQO_RYX(true, 2, 1, 24, 19),  // Lanczos-8 / -9 2:1
+        IQO_RYX(true, 9, 4, 12, 8, 2), IQO_RYX(true, 9, 4, 12, 10, 2),  // Lanczos-3 9:4 (1080p -> 480p, -> 640x480)
+        IQO_RYX(true, 9, 4, 8, 6, 2), IQO_RYX(true, 9, 4, 8, 7, 2),     // Lanczos-2 9:4
+        IQO_RYX(false, 9, 4, 4, 3, 2),                                  // Area 9:4
+        IQO_RYX(true, 4, 1, 14, 13, 2), IQO_RYX(true, 4, 1, 14, 9, 2),  // Lanczos-3 / -2 4:1 (4K -> 960x540)
+        IQO_RYX(true, 2, 1, 4, 3, 2),                                   // Lanczos-1 2:1
+        IQO_RYX(true, 2, 1, 12, 9, 3), IQO_RYX(true, 2, 1, 16, 11, 4),  // Lanczos-4 / -5 2:1
+        IQO_RYX(true, 2, 1, 18, 13, 5), IQO_RYX(true, 2, 1, 20, 15, 5), // Lanczos-6 / -7 2:1
+        IQO_RYX(true, 2, 1, 22, 17, 2), IQO_RYX(true, 2, 1, 24, 19, 2), // Lanczos-8 / -9 2:1
     };
 #undef IQO_RYX
     const void *kern = nullptr;
@@ -4820,7 +4902,7 @@ hipError_t launch_area_int(const AreaDev &g, const Io &io, int rowBegin, int row
 
 hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEnd, int bands, Prep<LinearArgs> *P)
 {
-    if (g.srcW % 8 || g.dstW != 2 * g.srcW || g.srcW < 8)
+    if (g.srcW % 8 || (g.F != 2 && g.F != 3) || g.dstW != g.F * g.srcW || g.srcW < 8)
         return hipErrorInvalidValue;
     const int rows = rowEnd - rowBegin;
     // producing lanes per wave: the fewest waves per row, then the fewest lanes that tile the width
@@ -4830,14 +4912,15 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
     wpr = (lanes + np - 1) / np;
     // nontemporal stores by default (variant builds: dbg 16 = plain stores, for A/B); 2 rows in
     // flight per wave measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
-    const bool nt = !(IQO_DBG(g) & 16);
-    const int pd = g.prefetch == 0 ? 2 : g.prefetch;
-    const void *kern = pd >= 8 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<8, true>)
-                                     : reinterpret_cast<const void *>(linear_up2_kernel<8, false>))
-                       : pd >= 4 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<4, true>)
-                                       : reinterpret_cast<const void *>(linear_up2_kernel<4, false>))
-                                 : (nt ? reinterpret_cast<const void *>(linear_up2_kernel<2, true>)
-                                       : reinterpret_cast<const void *>(linear_up2_kernel<2, false>));
+    const bool nt = g.F == 3 || !(IQO_DBG(g) & 16);
+    const int pd = g.prefetch == 0 || g.F == 3 ? 2 : g.prefetch;  // (3x: nontemporal, 2 ahead only)
+    const void *kern = g.F == 3  ? reinterpret_cast<const void *>(linear_up2_kernel<2, true, 3>)
+                       : pd >= 8 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<8, true, 2>)
+                                       : reinterpret_cast<const void *>(linear_up2_kernel<8, false, 2>))
+                       : pd >= 4 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<4, true, 2>)
+                                       : reinterpret_cast<const void *>(linear_up2_kernel<4, false, 2>))
+                                 : (nt ? reinterpret_cast<const void *>(linear_up2_kernel<2, true, 2>)
+                                       : reinterpret_cast<const void *>(linear_up2_kernel<2, false, 2>));
     if (bands <= 0) {
         // ~6 rounds of resident waves, >= 16 rows per band (fresh data, C4 x256: 48 bands 0.537 ms
         // vs 0.555 for the one-round makespan choice)
@@ -4972,7 +5055,7 @@ hipError_t launch_yuv420_linear(const LinearDev &gy, const Io &ioY, const Linear
         (e = prep_linear(gc, ioU, 0, gc.dstH, 0, &pu)) != hipSuccess ||
         (e = prep_linear(gc, ioV, 0, gc.dstH, 0, &pv)) != hipSuccess)
         return e;
-    if (py.kind != 1 || pu.kind != 1 || py.pd != 2 || pu.pd != 2)
+    if (py.kind != 1 || pu.kind != 1 || py.pd != 2 || pu.pd != 2 || gy.F != 2 || gc.F != 2)
         return hipErrorNotSupported;
     return launch_fused3(reinterpret_cast<const void *>(yuv420_plane_kernel<LinearPlane, LinearArgs>), py, pu, pv,
                          256, 0, s);

@@ -220,8 +220,9 @@ hipError_t launch_area_int(const AreaDev &a, const Io &io, int rowBegin, int row
 // --- exact 2x bilinear upsampler.
 struct LinearDev {
     int srcW, srcH, dstW, dstH;
-    uint32_t cy[2];              // per phase (c0, c1) u16 pairs
-    uint32_t cx[2];
+    int F;                       // exact factor, 2 or 3
+    uint32_t cy[3];              // per phase (c0, c1) u16 pairs
+    uint32_t cx[3];
     int dbg;                     // variant builds only: 16 = plain (not nontemporal) stores
     int prefetch;                // source rows in flight per wave (2, 4, 8; 0 = default 2)
     int np;                      // producing lanes per wave (0 = auto)

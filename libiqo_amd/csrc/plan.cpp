@@ -566,21 +566,27 @@ void pick_fast_area(Plan *p)
     p->kernel = 2;  // IQO_KERNEL_AREA_INT
 }
 
+// Linear at exactly 2x or 3x (kernels.hip linear_up2_kernel_body): main output F k + i (i = 1 .. F)
+// blends source samples k and k + 1 with phase (i % F)'s two taps (IQOLinearResizerImpl_Generic.cpp
+// :252-271 / :384-406, srcO = floor((y + 0.5) / F - 0.5)); the first and last output replicate the
+// edge sample (:240-248, :273-281, :343-345).
 void pick_fast_linear(Plan *p)
 {
     AxisPlan &x = p->x, &y = p->y;
-    if (x.identity || y.identity || p->dstW != 2 * p->srcW || p->dstH != 2 * p->srcH)
+    const int F = p->dstW == 3 * p->srcW ? 3 : 2;
+    if (x.identity || y.identity || p->dstW != F * p->srcW || p->dstH != F * p->srcH)
         return;
-    if (x.phases != 2 || y.phases != 2 || p->dstW % 16)
+    if (x.phases != F || y.phases != F || p->dstW % (8 * F))
         return;
     for (const AxisPlan *a : {&x, &y}) {
         if (a->mainBegin != 1 || a->mainEnd != a->dstLen - 1)
             return;
         for (int i = a->mainBegin; i < a->mainEnd; ++i)
-            if (a->coord[i].srcO != ((i - 1) >> 1) || a->coord[i].tabOff != (i % 2) * 2)
+            if (a->coord[i].srcO != (i - 1) / F || a->coord[i].tabOff != (i % F) * 2)
                 return;
     }
-    for (int q = 0; q < 2; ++q)
+    p->fln.F = F;
+    for (int q = 0; q < F; ++q)
         for (int k = 0; k < 2; ++k) {
             p->fln.cx[q][k] = static_cast<uint16_t>(x.table[2 * q + k]);
             p->fln.cy[q][k] = static_cast<uint16_t>(y.table[2 * q + k]);

@@ -89,7 +89,8 @@ struct FastArea {
 };
 
 struct FastLinear {
-    uint16_t cy[2][2] = {{0, 0}, {0, 0}}, cx[2][2] = {{0, 0}, {0, 0}};
+    int F = 2;  // exact factor (2 or 3): output F k + i (i = 1 .. F) blends samples k, k + 1, phase i % F
+    uint16_t cy[3][2] = {}, cx[3][2] = {};
 };
 
 struct Plan {

@@ -307,6 +307,40 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
         }
         return 0;
     }
+    if (kind == 8) {
+        // linear_up2_kernel_body (Linear exactly 2x / 3x): main row F k + i (i = 1 .. F) blends
+        // source rows k, k + 1 with phase i % F; main column x blends work columns m, m + 1,
+        // m = (x - 1) / F; edge rows take one source row at 256, edge columns (w * 2^15 + 2^22) >> 23
+        if (p.kernel != 3)
+            return 1;
+        const int F = p.fln.F;
+        for (int y = 0; y < dstH; ++y) {
+            int r0, c0, c1;
+            if (y == 0 || y == dstH - 1) {
+                r0 = y == 0 ? 0 : srcH - 1;
+                c0 = 256;
+                c1 = 0;
+            } else {
+                r0 = (y - 1) / F;
+                c0 = p.fln.cy[y % F][0];
+                c1 = p.fln.cy[y % F][1];
+            }
+            for (int c = 0; c < srcW; ++c)
+                work[static_cast<size_t>(c)] = static_cast<uint16_t>(px(r0, c) * c0 + (c1 ? px(r0 + 1, c) * c1 : 0));
+            for (int x = 0; x < dstW; ++x) {
+                uint32_t s;
+                if (x == 0 || x == dstW - 1)
+                    s = work[static_cast<size_t>(x == 0 ? 0 : srcW - 1)] * 32768u + (1u << 22);
+                else
+                    s = work[static_cast<size_t>((x - 1) / F)] * static_cast<uint32_t>(p.fln.cx[x % F][0]) +
+                        (p.fln.cx[x % F][1] ? work[static_cast<size_t>((x - 1) / F + 1)] * static_cast<uint32_t>(p.fln.cx[x % F][1]) : 0u) +
+                        (1u << 22);
+                const int v = static_cast<int>(s) >> 23;
+                dst[static_cast<size_t>(y) * dstW + x] = static_cast<uint8_t>(v > 255 ? 255 : v);
+            }
+        }
+        return 0;
+    }
     if (kind == 2) {
         A32Tables a;
         build_a32(p, &a);

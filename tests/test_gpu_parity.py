@@ -472,21 +472,25 @@ def test_tile_streamer_matches_oracle(cfg):
 
 
 LINEAR_UP2_SHAPES = [
-    (1920, 1080),  # C4: 4 waves x 60 lanes per row
-    (640, 480),    # 80 lanes: 2 waves x 40
-    (8, 1),        # one producing lane; both output rows are replicated borders
-    (24, 2),       # three lanes, one interior row pair
-    (504, 7),      # 63 lanes: 2 waves, the right-edge wave overlaps its neighbour
-    (1000, 33),
+    (1920, 1080, 2),  # C4: 4 waves x 60 lanes per row
+    (640, 480, 2),    # 80 lanes: 2 waves x 40
+    (8, 1, 2),        # one producing lane; both output rows are replicated borders
+    (24, 2, 2),       # three lanes, one interior row pair
+    (504, 7, 2),      # 63 lanes: 2 waves, the right-edge wave overlaps its neighbour
+    (1000, 33, 2),
+    (1280, 720, 3),   # 3x: 24 output columns per lane, 3 output rows per source row
+    (8, 1, 3),
+    (24, 3, 3),
+    (504, 7, 3),
 ]
 
 
-@pytest.mark.parametrize("shape", LINEAR_UP2_SHAPES, ids=lambda s: "%dx%d" % s)
+@pytest.mark.parametrize("shape", LINEAR_UP2_SHAPES, ids=lambda s: "%dx%dx%d" % s)
 def test_linear_up2_streamer_variants(shape):
-    """The exact-2x Linear streamer at every prefetch depth and band split (bands starting on odd
-    and even rows, one-row bands, bands holding only a border row) produces the oracle's output."""
-    sw, sh = shape
-    dw, dh = 2 * sw, 2 * sh
+    """The exact-2x / 3x Linear streamer at every prefetch depth and band split (bands starting on
+    any row phase, one-row bands, bands holding only a border row) produces the oracle's output."""
+    sw, sh, f = shape
+    dw, dh = f * sw, f * sh
     frames = _noise_batch(2, sw, sh, 500)
     frames[1, :, : max(1, sw // 5)] = 255
     src = torch.from_numpy(frames).to(DEV)

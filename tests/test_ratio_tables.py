@@ -17,7 +17,7 @@ import oracle_lib as ol
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
-KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6,
+KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6, "linear_up": 8,
          "linear_d2": 7}
 
 
@@ -81,6 +81,8 @@ def _shapes():
            ("linear_d2", "linear", 0, 32, 4, 16, 2), ("linear_d2", "linear", 0, 48, 6, 24, 3),
            ("lanczos_up2", "lanczos", 3, 1280, 720, 3840, 2160), ("lanczos_up2", "lanczos", 2, 640, 360, 1920, 1080),  # 3x
            ("lanczos_up2", "lanczos", 3, 16, 4, 48, 12), ("lanczos_up2", "lanczos", 2, 16, 5, 48, 15),
+           ("linear_up", "linear", 0, 1280, 720, 3840, 2160), ("linear_up", "linear", 0, 1920, 1080, 3840, 2160),
+           ("linear_up", "linear", 0, 8, 2, 24, 6), ("linear_up", "linear", 0, 16, 3, 32, 6),
            ("ryx", "lanczos", 3, 3840, 2160, 960, 540), ("ryx", "lanczos", 2, 1920, 1080, 480, 270),  # 4:1
            ("ryx", "lanczos", 1, 640, 480, 320, 240), ("ryx", "lanczos", 4, 1920, 1080, 960, 540),   # 2:1
            ("ryx", "lanczos", 5, 640, 360, 320, 180), ("ryx", "lanczos", 6, 640, 360, 320, 180),
@@ -98,6 +100,8 @@ def _shapes():
         out.append(("lanczos_d31", "lanczos", rng.choice((2, 3)), 12 * a + 48, 3 * b + 24, 4 * a + 16, b + 8))
         sw = 4 * rng.randint(20, 500)
         out.append(("linear_d2", "linear", 0, 16 * a, 2 * b, 8 * a, b))
+        f = rng.choice((2, 3))
+        out.append(("linear_up", "linear", 0, 8 * a, b, f * 8 * a, f * b))
         out.append(("ryx", rng.choice(("lanczos", "area")), 3, sw, 9 * b + 36,
                     2 * rng.randint(sw // 4 + 1, min(1024, sw) // 2) - rng.randint(0, 1), 4 * b + 16))
         out.append(("ryx", "lanczos", rng.choice((1, 4, 5, 6, 7, 8, 9)), sw, 2 * b + 40, sw // 2, b + 20))
