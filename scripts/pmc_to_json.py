@@ -23,7 +23,9 @@ KERNELS = {"lanczos_stream": "lanczos_s", "area_int": "area_int_kernel",  # lanc
            "area_d32": "area_d32_kernel", "lanczos_d31": "lanczos_d31_kernel", "ryx": "ryx_kernel"}
 BENCH = {"c2": ("lanczos_stream", 256), "c3": ("area_int", 64), "c4": ("linear_up2", 256), "c1": ("lanczos_stream", 4096),
          "g1": ("lanczos_d32", 128), "g2": ("lanczos_up2", 32), "g3": ("area_d32", 128),
-         "g4": ("lanczos_d31", 128), "g5": ("ryx", 256), "g6": ("area_int", 128)}
+         "g4": ("lanczos_d31", 128), "g5": ("ryx", 256), "g6": ("area_int", 128),
+         "h1": ("area_int", 128, "linear_d2_kernel"), "h2": ("ryx", 128), "h3": ("ryx", 128), "h4": ("lanczos_up2", 64),
+         "h5": ("linear_up2", 64), "h6": ("ryx", 128)}
 
 
 def per_dispatch(dirname, counter, kname):
@@ -48,8 +50,8 @@ def main():
     out_dir, cfgs = args[0], args[1:]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for c in cfgs:
-        kernel, frames = BENCH[c]
-        kname = KERNELS[kernel]
+        kernel, frames = BENCH[c][:2]
+        kname = BENCH[c][2] if len(BENCH[c]) > 2 else KERNELS[kernel]  # (Linear 2:1 runs area_int's linear_d2_kernel)
         fetch = per_dispatch(os.path.join(out_dir, "pmc_fetch_" + c), "FETCH_SIZE", kname)
         write = per_dispatch(os.path.join(out_dir, "pmc_write_" + c), "WRITE_SIZE", kname)
         if not fetch or not write:
