@@ -737,6 +737,8 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.tail = h->tail;
     l.stack = h->stack;
     l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
+    if (f.NY == 12)
+        l.sym = 1;  // Lanczos-4 2:1: the block-shared symmetric streamer is its only instantiation
     l.NX = f.NX;
     l.offXO = f.offXO;
     for (int i = 0; i < f.NX / 2 && i < 8; ++i)

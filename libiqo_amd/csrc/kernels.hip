@@ -1531,7 +1531,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
 template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, bool LINE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void lanczos_symb_kernel(LanczosArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 10 ? 3 : 4))) void lanczos_symb_kernel(LanczosArgs a)
 {
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int rpb = a.rowsPerBand;
@@ -4703,6 +4703,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
         np = l.np > 0 ? min(l.np, 62) : (lanes + wpr - 1) / wpr;
         if (np * 8 > l.dstW)
             np = l.dstW / 8;
+        if (l.NY == 12 && (l.dstW + 8 * np - 1) / (8 * np) > 4)
+            np = (lanes + wpr - 1) / wpr;  // (a lane count that needs more than 4 waves: the default)
         opw = 8 * np;
         wpr = (l.dstW + opw - 1) / opw;
     }
@@ -4719,6 +4721,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int lastLanes = (rowNeed - 16 - 1024 * (chunks - 1)) / 16;
     const int cpw = (chunks + wpr - 1) / wpr;
     const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
+    if (l.NY == 12 && !shared)
+        return hipErrorInvalidValue;  // Lanczos-4 2:1: block-shared instantiation only (plan.cpp)
     // narrow frames: several frames side by side in one 2-wave workgroup (lanczos_stack_kernel)
     const int npf = l.srcW / 16;
     const int fpwMax = npf >= 1 ? std::min(6, 125 / (npf + 1)) : 0;
@@ -4726,13 +4730,13 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     // 0.427 vs 0.529 ms per 16384 frames; at 3 frames of 640 columns (C1) it is no faster, and 3.5 %
     // slower for Lanczos-3 640x360 -> 320x180, profiles/r03/stack_narrow.txt; option "stack" = 2
     // forces it from 2 frames per workgroup)
-    const bool stack = shared && l.stack && wpr == 1 && l.srcW == 2 * l.dstW && l.srcW % 16 == 0 && np == npf &&
+    const bool stack = shared && l.NY <= 10 && l.stack && wpr == 1 && l.srcW == 2 * l.dstW && l.srcW % 16 == 0 && np == npf &&
                        fpwMax >= (l.stack >= 2 ? 2 : 4) && io.frames >= 2;
     // block-shared ring depth: prefetch 1-2 -> 3, 3 (default) -> the window period NY/2 (4 for
     // Lanczos-2, 5 for Lanczos-3: every ring slot index is then a compile-time constant; C2 x256
     // 0.5226 vs 0.532 ms at depth 4), 4 -> 5.  Depth 5 packs the ring rows to the bytes they need
     // so that four 4-wave workgroups still fit a CU's LDS.
-    const int K = pd <= 2 ? 3 : pd == 3 ? (l.NY == 10 ? 5 : 4) : 5;
+    const int K = pd <= 2 ? 3 : pd == 3 ? (l.NY >= 10 ? 5 : 4) : 5;
     const bool pack = l.ringPack || (shared && K == 5);
     const int rowPitch = pack ? rowNeed : 16 + 1024 * chunks;
     int fpw = 1;
@@ -4771,6 +4775,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             kern = IQO_SYMB(10, 12, -5, true);
         else if (l.NY == 10)
             kern = IQO_SYMB(10, 12, -5, false);
+        else if (l.NY == 12)
+            kern = IQO_SYMB(12, 16, -7, false);  // Lanczos-4 2:1 (3 waves per SIMD: the 12-row window)
         else
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB

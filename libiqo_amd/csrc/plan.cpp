@@ -533,6 +533,10 @@ void pick_fast_lanczos(Plan *p)
     bool inst = KY == 2 && KX == 2 && ((f.NY == 10 && f.NXP == 14 && f.offX == -6) ||
                                        (f.NY == 8 && f.NXP == 10 && f.offX == -4) ||
                                        (f.NY == 4 && f.NXP == 4 && f.offX == 0));
+    // Lanczos-4 2:1 (12 non-zero Y taps, 16 X taps from 2x - 7): the block-shared symmetric
+    // streamer only (no ring-streamer instantiation), so only where that one runs: <= 4 waves of
+    // 62 producing lanes per row, symmetric Y taps, no negative denominators
+    const bool l4 = KY == 2 && KX == 2 && f.NY == 12 && (xh - xl) == 16 && off == -7 && p->dstW <= 4 * 62 * 8;
     // symmetric variant: (NY, NX, offXO) = (10, 12, -5) Lanczos-3 2:1, (8, 8, -3) Lanczos-2 2:1
     f.NX = xh - xl;
     f.offXO = off;
@@ -540,7 +544,11 @@ void pick_fast_lanczos(Plan *p)
     bool symY = (f.NY % 2) == 0;
     for (int i = 0; symY && i < f.NY / 2; ++i)
         symY = f.cy[static_cast<size_t>(i)] == f.cy[static_cast<size_t>(f.NY - 1 - i)];
-    f.sym = inst && symY && (off & 1) && !f.yTopNeg && !f.yBotNeg && !f.xNeg && ((f.NY == 10 && f.NX == 12 && off == -5) || (f.NY == 8 && f.NX == 8 && off == -3));
+    f.sym = (inst || l4) && symY && (off & 1) && !f.yTopNeg && !f.yBotNeg && !f.xNeg &&
+            ((f.NY == 10 && f.NX == 12 && off == -5) || (f.NY == 8 && f.NX == 8 && off == -3) ||
+             (f.NY == 12 && f.NX == 16 && off == -7));
+    if (l4 && f.sym)
+        inst = true;
     if (!inst || (p->srcW % 16) || p->srcW > 8192)
         return;
     p->kernel = 1;  // IQO_KERNEL_LANCZOS_STREAM

@@ -328,6 +328,10 @@ STREAM_SHAPES = [
     (3, 1936, 1090, 968, 545),    # odd output height, right-edge wave overlaps its neighbour
     (3, 4000, 64, 2000, 32),      # short bands, 5 waves per row
     (2, 2064, 40, 1032, 20),
+    (4, 3840, 2160, 1920, 1080),  # Lanczos-4 2:1: block-shared symmetric streamer (12-row window)
+    (4, 1936, 1090, 968, 545),
+    (4, 640, 480, 320, 240),
+    (4, 2064, 40, 1032, 20),
 ]
 
 
@@ -1194,7 +1198,8 @@ RYX_SHAPES = [
     ("lanczos", 3, 3840, 2160, 960, 540, 1),     # 4:1 (14 of 24 row taps, 13 pairs), two 512-thread parts
     ("lanczos", 2, 1920, 1080, 480, 270, 1),     # 4:1 (14 of 16 row taps)
     ("lanczos", 1, 1280, 720, 640, 360, 1),      # 2:1 Lanczos-1
-    ("lanczos", 4, 1920, 1080, 960, 540, 1),     # 2:1 Lanczos-4 .. -9: 12 .. 24 row taps
+    ("lanczos", 4, 4096, 1080, 2048, 540, 1),    # 2:1 Lanczos-4 .. -9: 12 .. 24 row taps (Lanczos-4 wider
+                                                 # than the symmetric streamer's 4 waves per row)
     ("lanczos", 5, 1280, 720, 640, 360, 1),
     ("lanczos", 6, 1280, 720, 639, 360, 1),
     ("lanczos", 7, 720, 480, 360, 240, 1),
