@@ -925,7 +925,7 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // column split into `n` workgroups of `threads` threads: output columns [xs[k], xs[k+1]) (even,
     // 2 per thread) from source columns [cs[k], ce[k]) (multiples of 4, 4 per thread)
     auto split = [&](int n, int threads) -> bool {
-        int xs[5], cs[4], ce[4];
+        int xs[17], cs[16], ce[16];
         for (int k = 0; k <= n; ++k)
             xs[k] = k == 0 ? 0 : k == n ? d.dstW : (k * d.dstW / n + 1) & ~1;
         for (int k = 0; k < n; ++k) {
@@ -943,26 +943,35 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
         }
         d.parts = n;
         d.threads = threads;
-        for (int k = 0; k < 5; ++k)
+        for (int k = 0; k < 17; ++k)
             d.xs[k] = k <= n ? xs[k] : d.dstW;
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 16; ++k) {
             d.cs[k] = k < n ? cs[k] : 0;
             d.ce[k] = k < n ? ce[k] : d.srcW;
         }
         return true;
     };
-    // Lanczos: two workgroups per row (4 waves each, half the columns) when each half's source
-    // span fits 256 threads x 4 columns: barriers over 4 waves instead of 8 (1080p -> 480p:
-    // Lanczos-2 0.171 vs 0.182 ms, Lanczos-3 0.232 vs 0.239; Area 5 % slower, so not for Area;
-    // profiles/r03/ryx_split.txt; option "ryx_split" = 0: off, 2: four 2-wave workgroups).  Rows
-    // wider than 512 threads x 4 columns take 2 or 4 parts of 512 threads.  parts = 0: no split
-    // fits (build_plan then drops the kernel).
+    // the fewest parts of `threads` threads that hold the row (up to 16)
+    auto split_min = [&](int threads) {
+        for (int n = 1; n <= 16; ++n)
+            if (split(n, threads))
+                return true;
+        return false;
+    };
+    // Lanczos: workgroups of 4 waves (half or a quarter of the row each) when their source spans
+    // fit 256 threads x 4 columns: barriers over 4 waves instead of 8 (1080p -> 480p: Lanczos-2
+    // 0.171 vs 0.182 ms, Lanczos-3 0.232 vs 0.239, profiles/r03/ryx_split.txt; 4K -> 960x540
+    // Lanczos-3 0.441 vs 0.404 ms with four parts instead of two of 8 waves; Area 5 % slower,
+    // so not for Area).  Option "ryx_split": 0 one 8-wave workgroup per row where it fits, 2 / 3
+    // parts of 2 waves / 1 wave.  parts = 0: no split fits (build_plan then drops the kernel).
     d.parts = 0;
     d.threads = 512;
-    const int n0 = h->ryxSplit >= 2 ? 4 : 2;
-    if (!(h->ryxSplit && d.lanczos && d.dstW >= 32 * n0 && split(n0, 512 / n0)) && !split(1, 512) &&
-        !split(2, 512))
-        split(4, 512);
+    const int tw = h->ryxSplit == 2 ? 128 : h->ryxSplit == 3 ? 64 : 256;
+    if (h->ryxSplit >= 2 && split_min(tw))
+        return d;
+    if (!(h->ryxSplit == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
+        !(h->ryxSplit == 1 && split(4, 256)))
+        split_min(512);
     return d;
 }
 
@@ -1319,8 +1328,8 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->rounds = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "ryx_split")) {  // ratio-Y kernel: 0 / 1 / 2: one / two / four workgroups per row (speed only)
-        if (value < 0 || value > 2)
+    if (!std::strcmp(key, "ryx_split")) {  // ratio-Y kernel column parts (speed only): 0 one 8-wave
+        if (value < 0 || value > 3)          // workgroup per row where it fits, 1 default, 2 / 3 parts of 2 / 1 waves
             return IQO_HIP_EINVAL;
         h->ryxSplit = static_cast<int>(value);
         return IQO_HIP_OK;

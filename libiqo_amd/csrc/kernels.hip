@@ -4488,7 +4488,7 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         IQO_RYX(true, 9, 4, 12, 8, 2), IQO_RYX(true, 9, 4, 12, 10, 2),  // Lanczos-3 9:4 (1080p -> 480p, -> 640x480)
         IQO_RYX(true, 9, 4, 8, 6, 2), IQO_RYX(true, 9, 4, 8, 7, 2),     // Lanczos-2 9:4
         IQO_RYX(false, 9, 4, 4, 3, 2),                                  // Area 9:4
-        IQO_RYX(true, 4, 1, 14, 13, 2), IQO_RYX(true, 4, 1, 14, 9, 2),  // Lanczos-3 / -2 4:1 (4K -> 960x540)
+        IQO_RYX(true, 4, 1, 14, 13, 4), IQO_RYX(true, 4, 1, 14, 9, 4),  // Lanczos-3 / -2 4:1 (4K -> 960x540)
         IQO_RYX(true, 2, 1, 4, 3, 2),                                   // Lanczos-1 2:1
         IQO_RYX(true, 2, 1, 12, 9, 3), IQO_RYX(true, 2, 1, 16, 11, 4),  // Lanczos-4 / -5 2:1
         IQO_RYX(true, 2, 1, 18, 13, 5), IQO_RYX(true, 2, 1, 20, 15, 5), // Lanczos-6 / -7 2:1
@@ -4506,10 +4506,10 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         }
     if (!kern)
         return hipErrorInvalidValue;
-    if (d.parts != 1 && d.parts != 2 && d.parts != 4)
+    if (d.parts < 1 || d.parts > 16)
         return hipErrorInvalidValue;
-    const int threads = d.threads > 0 ? d.threads : 512 / d.parts;
-    if (threads % 64 || threads > 512 || threads * d.parts > 2048)
+    const int threads = d.threads > 0 ? d.threads : 512;
+    if (threads % 64 || threads > 512)
         return hipErrorInvalidValue;
     int maxSpan = d.srcW;
     if (d.parts > 1) {

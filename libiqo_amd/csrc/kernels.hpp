@@ -132,10 +132,9 @@ struct RyxDev {
     const uint32_t *colCoef;     // dstW x NP pairs
     // column split: `parts` workgroups per (band, frame), part k writes output columns
     // [xs[k], xs[k+1]) from source columns [cs[k], ce[k]) (multiples of 4); parts = 1: the whole row
-    int parts;                   // 1, 2 or 4
-    int threads;                 // threads per workgroup (4 source columns each): 512 / parts, or 512
-                                 // when the source is wider than 2048 columns (parts of 512 threads)
-    int xs[5], cs[4], ce[4];
+    int parts;                   // 1 .. 16
+    int threads;                 // threads per workgroup (4 source columns each, a multiple of 64)
+    int xs[17], cs[16], ce[16];
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
