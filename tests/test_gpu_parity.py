@@ -1438,3 +1438,39 @@ def test_plan_cache_resets_options():
         assert (_run_host(r2, frame, dw, dh) == exp).all()
         del r2
         gc.collect()
+
+
+def _fuzz_shapes():
+    """Seeded random shapes over the round-4 kernel families and the general kernels."""
+    import random
+    rng = random.Random(404)
+    out = []
+    for _ in range(12):
+        a, b = rng.randint(4, 60), rng.randint(4, 40)
+        out.append(("lanczos", rng.choice((1, 4, 4, 5, 6, 7, 8, 9)), 16 * a, 2 * b + 24, 8 * a, b + 12))  # 2:1
+        out.append(("lanczos", rng.choice((2, 3)), 32 * a, 4 * b + 32, 8 * a, b + 8))                   # 4:1
+        out.append(("lanczos", rng.choice((2, 3)), 8 * a, b + 8, 24 * a, 3 * b + 24))                   # 3x
+        out.append(("linear", 0, 8 * a, b + 2, 24 * a, 3 * b + 6))                                       # 3x
+        out.append(("linear", 0, 16 * a, 2 * b + 2, 8 * a, b + 1))                                       # 2:1
+        sw = 4 * rng.randint(20, 300)
+        out.append(("lanczos", rng.choice((2, 3)), sw, 9 * b + 36, rng.randint(sw // 4, sw), 4 * b + 16))  # 9:4 rows
+        out.append((rng.choice(("lanczos", "area", "linear")), rng.randint(2, 4), rng.randint(40, 900),
+                    rng.randint(20, 300), rng.randint(30, 1200), rng.randint(16, 400)))                 # general
+    return out
+
+
+@pytest.mark.parametrize("cfg", _fuzz_shapes(), ids=lambda c: "%s%d_%dx%d_%dx%d" % c)
+def test_random_shapes_match_oracle(cfg):
+    """Seeded random shapes over every kernel family (whichever kernel the plan picks): two frames
+    of noise and one half-flat frame, device batch vs the oracle, bit for bit."""
+    m, d, sw, sh, dw, dh = cfg
+    if m == "linear" and (dw > 2 * sw or dh > 2 * sh) and (dw != 3 * sw or dh != 3 * sh):
+        pytest.skip("Linear upsampling beyond 2x reads outside the reference's row (SURVEY 8a quirks)")
+    frames = _noise_batch(3, sw, sh, 9000 + sw + sh)
+    frames[2, :, sw // 2:] = 255
+    exp = [ol.run_oracle(m, d, sw, sh, dw, dh, 1, frames[f]) for f in range(3)]
+    r = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, 1)
+    out = r.resize_tensor(torch.from_numpy(frames).to(DEV)).cpu().numpy()
+    for f in range(3):
+        bad = np.argwhere(out[f] != exp[f])
+        assert bad.size == 0, (cfg, r.describe()["kernel"], f, bad[:4].tolist())
