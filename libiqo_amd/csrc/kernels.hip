@@ -3309,17 +3309,18 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
 //   / IQOAreaResizerImpl_Generic.cpp:271-293 row loops): packed MACs, 16-bit wrap; masked Lanczos
 //   border rows (rows outside the image load as zero) are divided in place (:464-490).
 // * The work row goes to LDS (u16, zero padding either side, double-buffered: one barrier per row).
-// * Horizontal: thread t computes output columns 2t, 2t + 1 from the table: NP coefficient pairs in
-//   VGPRs for the whole band, NP dword reads from the work row at the column's even window start,
-//   v_dot2 (:582-612 / :340-368); Lanczos columns end in an exact multiply-high division (the
-//   identity 2^20 in the interior, the border divisor of :539-574 at the edges).
+// * Horizontal: thread t computes output columns t and half + t of its part from the table (one
+//   column apart in neighbouring lanes: the work-row reads spread over the LDS banks; 4:1 also
+//   rotates the reads of lanes 16-31 of each half by one pair): NP coefficient pairs in VGPRs for
+//   the whole band, NP dword reads from the work row at the column's even window start, v_dot2
+//   (:582-612 / :340-368); Lanczos columns end in an exact multiply-high division (the identity
+//   2^20 in the interior, the border divisor of :539-574 at the edges); one byte store per column.
 struct RyxArgs {
     RyxDev d;
     Io io;
     int rowBegin, rowEnd, groupBegin, rowsPerBand, bands;
     int srcBytes, dstBytes;
     unsigned nBlocks;
-    int byteStores;  // destination not 2-byte aligned (base or strides): two 1-byte stores per thread
 };
 
 #ifndef IQO_RYX_WPE
@@ -3382,14 +3383,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * span + 4 * k) = 0u;
     }
     // this thread's two output columns: table entries for the whole band
-    const int x0 = xLo + 2 * t;
+    // Thread t owns output columns xLo + t and xLo + half + t: neighbouring lanes read windows
+    // one output column apart, so the work-row reads spread over the LDS banks (columns 2t, 2t + 1
+    // put 4:1 lanes 16 B apart: 8-way bank conflicts, 56 % of the LDS cycles; 9:4 44 %)
+    const int half = (xHi - xLo + 1) >> 1;
+    const int xc[2] = {xLo + t, xLo + half + t};
     uint32_t cf[2][NP];
     int aoff[2];
     uint32_t mm[2];
     int sh[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const int x = min(x0 + k, xHi - 1);
+        const int x = min(xc[k], xHi - 1);
         const int4 c = d.cols[x];
         aoff[k] = c.x - 2 * cLo;  // work-row byte offset relative to this part's first column
         mm[k] = static_cast<uint32_t>(c.y);
@@ -3398,16 +3403,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
         for (int q = 0; q < NP; ++q)
             cf[k][q] = d.colCoef[x * NP + q];
     }
+    // 4:1: neighbouring lanes' windows are 2 dwords apart, so lanes t and t + 16 of a 32-lane half
+    // meet on one bank (ds_read_b32 / ds_read2: bank = dword mod 32).  Lanes 16-31 of each half read
+    // their window rotated by one pair (pair q + 1 first, pair 0 last): every read of a half then
+    // touches 32 distinct banks.  The coefficient pairs are rotated the same way, once.
+    constexpr bool ROT = P == 4 && Q == 1;
+    const int rot = ROT ? (t >> 4) & 1 : 0;
+    int aoffB[2];  // byte offset of the last pair read (aoff[k] + 4 rot + 4 q for the others)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if constexpr (ROT) {
+            const uint32_t c0 = cf[k][0];
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+                cf[k][q] = rot ? (q + 1 < NP ? cf[k][q + 1] : c0) : cf[k][q];
+        }
+        aoffB[k] = rot ? aoff[k] : aoff[k] + 4 * (NP - 1);
+        aoff[k] += 4 * rot;
+    }
     // interior Lanczos columns divide by 2^20 (magic_x: m = 2^31, shift 19), which is one
     // saturating pack of both columns; only the few border columns take the exact division
     const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
-    // part bounds are even (launch_ryx) except an odd output width's end: its last thread has one
-    // column and stores one byte (so does every thread, twice, when the destination is not 2-byte
-    // aligned); uniform per workgroup
-    const bool pair = x0 + 1 < xHi;
-    const bool bytes = a.byteStores != 0, oddEnd = (xHi & 1) != 0;
-    const int stoff = x0 < xHi && (pair || bytes) && IQO_RYX_EXP != 2 ? x0 : OOB;
-    const int stoff1 = bytes ? (pair && IQO_RYX_EXP != 2 ? x0 + 1 : OOB) : (x0 < xHi && !pair ? x0 : OOB);
+    // one byte store per column (a wave stores 64 consecutive bytes per instruction)
+    const int stoff = t < half && IQO_RYX_EXP != 2 ? xc[0] : OOB;
+    const int stoff1 = t < half && xc[1] < xHi && IQO_RYX_EXP != 2 ? xc[1] : OOB;
 
     // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1.
     // Rows outside the image load as zero (the reference's masked border sums); rows past the
@@ -3512,7 +3531,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
             for (int k = 0; k < 2; ++k)
 #pragma unroll
                 for (int q = 0; q < NP; ++q)
-                    w[k][q] = reinterpret_cast<const uint32_t *>(wr + aoff[k])[q];
+                    w[k][q] = q + 1 < NP ? reinterpret_cast<const uint32_t *>(wr + aoff[k])[q]
+                                         : *reinterpret_cast<const uint32_t *>(wr + aoffB[k]);
             // the next row's vertical pass (the next trip's first row after the trip's last)
             auto next_vertical = [&]() {
                 const int gn = base + (r + 1) / Q;
@@ -3559,14 +3579,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
             }
             const bool ok = y >= y0 && y < y1;
             const int rowOff = ok ? (y - dstRow0) * dstSt : OOB;
-            if (bytes) {
-                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff + rowOff, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed >> 8), dstR, stoff1 + rowOff, 0, 0);
-            } else {
-                __builtin_amdgcn_raw_buffer_store_b16(static_cast<uint16_t>(packed), dstR, stoff + rowOff, 0, 0);
-                if (oddEnd)
-                    __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff1 + rowOff, 0, 0);
-            }
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff + rowOff, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed >> 8), dstR, stoff1 + rowOff, 0, 0);
             if constexpr (!PIPE)
                 next_vertical();
         });
@@ -4543,11 +4557,8 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames) * static_cast<uint64_t>(d.parts);
     if (nBlocks >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
-    // 2-byte stores need an even destination base and even strides; otherwise 1-byte stores
-    const int byteStores = ((reinterpret_cast<uintptr_t>(io.dst) | static_cast<uintptr_t>(io.dstSt) |
-                             static_cast<uintptr_t>(io.dstFrameSt)) & 1) != 0;
     RyxArgs a{d, io, rowBegin, rowEnd, groupBegin, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
-              static_cast<unsigned>(nBlocks), byteStores};
+              static_cast<unsigned>(nBlocks)};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(static_cast<unsigned>(threads)), args,
                            static_cast<size_t>(ldsBytes), s);
