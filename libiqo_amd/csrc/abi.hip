@@ -727,6 +727,12 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
         l.xM[k] = f.xM[k];
         l.xT[k] = f.xT[k];
     }
+    if (f.NX == 20 && f.NY == 16) {  // Lanczos-5 2:1: kernels.hpp LanczosDev (reused fields)
+        for (int k = 0; k < 16; ++k) {
+            l.cx[k] = f.xM8[k];
+            (k < 8 ? l.xM[k] : reinterpret_cast<uint32_t &>(l.xT[k - 8])) = static_cast<uint32_t>(f.xT8[k]);
+        }
+    }
     l.yTopNeg = f.yTopNeg;
     l.yBotNeg = f.yBotNeg;
     l.xNeg = f.xNeg;
@@ -737,12 +743,12 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.tail = h->tail;
     l.stack = h->stack;
     l.sym = !f.sym || h->streamVariant == 1 ? 0 : (h->streamVariant >= 2 ? h->streamVariant : 1);
-    if (f.NY == 12)
-        l.sym = 1;  // Lanczos-4 2:1: the block-shared symmetric streamer is its only instantiation
+    if (f.NY == 12 || f.NY == 16)
+        l.sym = 1;  // Lanczos-4 / -5 2:1: the block-shared symmetric streamer is their only instantiation
     l.NX = f.NX;
     l.offXO = f.offXO;
-    for (int i = 0; i < f.NX / 2 && i < 8; ++i)
-        l.cxo[i] = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);
+    for (int i = 0; i < f.NX / 2 && i < 10; ++i)
+        (i < 8 ? l.cxo[i] : l.cy[i]) = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);  // (pairs 8, 9: Lanczos-5)
     l.np = h->lanes;
     l.xcd = h->xcdOrder;
     return l;

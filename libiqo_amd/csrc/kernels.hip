@@ -880,10 +880,12 @@ __device__ __forceinline__ void dma_row_masked(uint32_t lds, int voff, __amdgpu_
 inline __host__ __device__ bool symb_line(int dstW, int np) { return dstW >= 256 && np >= 16; }
 // LDS bytes of the block-shared streamer's edge area (after the ring): the line scheme's parked
 // pieces and sums of one trip of NY/2 rows, or the narrow-row scheme's sums
-constexpr int symb_edge_bytes(int NY)
+// (NX > 16, Lanczos-5: 8 border sums per row and side)
+constexpr int symb_edge_bytes(int NY, int NX)
 {
-    return 2 * (NY / 2) * (128 + 16) > 2 * IQO_SYMB_EDGE_BATCH * 16 ? 2 * (NY / 2) * (128 + 16)
-                                                                     : 2 * IQO_SYMB_EDGE_BATCH * 16;
+    return 2 * (NY / 2) * (128 + (NX > 16 ? 32 : 16)) > 2 * IQO_SYMB_EDGE_BATCH * 16
+               ? 2 * (NY / 2) * (128 + (NX > 16 ? 32 : 16))
+               : 2 * IQO_SYMB_EDGE_BATCH * 16;
 }
 __device__ __forceinline__ void dma_row_nt(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff)
 {
@@ -894,6 +896,10 @@ __device__ __forceinline__ void dma_row_nt(uint32_t lds, int voff, __amdgpu_buff
                  : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
                  : "memory");
 }
+
+// X coefficient pair p of the symmetric streamers (pairs 8, 9 of Lanczos-5 live in cy[8], cy[9]:
+// kernels.hpp LanczosDev)
+__device__ __forceinline__ uint32_t cxo_at(const LanczosDev &L, int p) { return p < 8 ? L.cxo[p] : L.cy[p]; }
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt()
@@ -1171,13 +1177,16 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     constexpr int EB = IQO_SYMB_EDGE_BATCH;
     static_assert((EB & (EB - 1)) == 0 && EB <= 64, "edge batch: power of two <= 64");
     static_assert(H <= 8, "line-scheme flush: 4 rows per 8-B store, two stores");
+    // Lanczos-5 (20 X taps): 5 border columns per side, so the edge lane parks all 8 of its sums
+    // and the flush divides 8 bytes per side (L.xM8: identity for the interior ones)
+    constexpr bool E8 = NX > 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int rowPitch = a.rowPitch, slotBytes = 2 * rowPitch;
     uint8_t *const ring = lds;
     int4 (*const edgeSum)[EB] = reinterpret_cast<int4 (*)[EB]>(lds + K * slotBytes);
     uint8_t *const lineBuf = lds + K * slotBytes;                                      // [2][H][128]
-    int4 *const lineSum = reinterpret_cast<int4 *>(lds + K * slotBytes + 2 * H * 128); // [2][H]
-    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + symb_edge_bytes(NY));
+    int4 *const lineSum = reinterpret_cast<int4 *>(lds + K * slotBytes + 2 * H * 128); // [2][H] (E8: [2][H][2])
+    const uint32_t sinkLds = static_cast<uint32_t>(K * slotBytes + symb_edge_bytes(NY, NX));
     // the last chunk of a row DMAs only its first lastLanes lanes (the row's pitch ends there)
     const int lastLanes = a.lastLanes > 0 && a.lastLanes < 64 ? a.lastLanes : 64;
     const uint64_t lastMask = lastLanes == 64 ? ~0ull : (1ull << lastLanes) - 1ull;
@@ -1238,7 +1247,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     uint32_t cvx[NX / 2];  // X coefficient pairs in VGPRs (the VOP2 DPP dot needs a VGPR src1)
 #pragma unroll
     for (int p = 0; p < NX / 2; ++p)
-        cvx[p] = opaque(L.cxo[p]);
+        cvx[p] = opaque(cxo_at(L, p));
 
     // shared LDS ring: iteration i's two walk rows live in slot i mod K; chunk c (1 KiB of
     // source columns [1024c, 1024c + 1024) at LDS column 16 + 1024c) is DMA'd by wave c mod wpr
@@ -1338,10 +1347,26 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             if (!(side ? edgeR : edgeL))
                 continue;  // uniform
             if (lane < n) {
-                const int4 e = lineSum[side * H + lane];
-                const uint32_t w = fix(e.x, 4 * side) | (fix(e.y, 4 * side + 1) << 8) | (fix(e.z, 4 * side + 2) << 16) |
-                                   (fix(e.w, 4 * side + 3) << 24);
-                *reinterpret_cast<uint32_t *>(lineBuf + (side * H + lane) * 128 + (side ? 124 : 0)) = w;
+                if constexpr (E8) {
+                    auto fix8 = [&](int sv, int k) {
+                        // (Lanczos-5's 16 edge constants: kernels.hpp LanczosDev)
+                        const uint32_t sh8 = k < 8 ? L.xM[k] : static_cast<uint32_t>(L.xT[k - 8]);
+                        const uint32_t qq = __umulhi(static_cast<uint32_t>(max(sv, 0)), L.cx[k]) >> sh8;
+                        return min(qq, 255u);
+                    };
+                    const int4 e0 = lineSum[2 * (side * H + lane)], e1 = lineSum[2 * (side * H + lane) + 1];
+                    const int k0 = 8 * side;
+                    const uint32_t w0 = fix8(e0.x, k0) | (fix8(e0.y, k0 + 1) << 8) | (fix8(e0.z, k0 + 2) << 16) |
+                                        (fix8(e0.w, k0 + 3) << 24);
+                    const uint32_t w1 = fix8(e1.x, k0 + 4) | (fix8(e1.y, k0 + 5) << 8) | (fix8(e1.z, k0 + 6) << 16) |
+                                        (fix8(e1.w, k0 + 7) << 24);
+                    *reinterpret_cast<u32x2 *>(lineBuf + (side * H + lane) * 128 + (side ? 120 : 0)) = u32x2{w0, w1};
+                } else {
+                    const int4 e = lineSum[side * H + lane];
+                    const uint32_t w = fix(e.x, 4 * side) | (fix(e.y, 4 * side + 1) << 8) |
+                                       (fix(e.z, 4 * side + 2) << 16) | (fix(e.w, 4 * side + 3) << 24);
+                    *reinterpret_cast<uint32_t *>(lineBuf + (side * H + lane) * 128 + (side ? 124 : 0)) = w;
+                }
             }
             const int colBase = side ? L.dstW - 128 : 0;
 #pragma unroll
@@ -1471,7 +1496,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                     pFirst = p;
             }
             int sacc;
-            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(L.cxo[pFirst]), "v"(acc[k + pFirst + JLO - 1]),
+            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(sacc) : "s"(cxo_at(L, pFirst)), "v"(acc[k + pFirst + JLO - 1]),
                 "v"(bias));
 #pragma unroll
             for (int p = 0; p < NX / 2; ++p) {
@@ -1485,7 +1510,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
                     asm("v_dot2c_i32_i16_dpp %0, %1, %2 wave_shl:1 row_mask:0xf bank_mask:0xf"
                         : "+v"(sacc) : "v"(acc[j - 9]), "v"(cvx[p]));
                 else
-                    sacc = sdot2(acc[j - 1], L.cxo[p], sacc);
+                    sacc = sdot2(acc[j - 1], cxo_at(L, p), sacc);
             }
             sum[k] = sacc;
         }
@@ -1497,10 +1522,21 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
             // line scheme: slot v of the trip (its first row is iteration base, slot 0)
             if (parkOff >= 0)
                 *reinterpret_cast<u32x2 *>(lineBuf + parkOff + v * 128) = o;
-            if (edgeL && laneL)  // (a wave whose x0 is not 0 can still have a lane at outX == dstW - 8)
-                lineSum[v] = make_int4(sum[0], sum[1], sum[2], sum[3]);
-            if (edgeR && laneR)
-                lineSum[H + v] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+            if constexpr (E8) {
+                if (edgeL && laneL) {
+                    lineSum[2 * v] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+                    lineSum[2 * v + 1] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+                }
+                if (edgeR && laneR) {
+                    lineSum[2 * (H + v)] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+                    lineSum[2 * (H + v) + 1] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+                }
+            } else {
+                if (edgeL && laneL)  // (a wave whose x0 is not 0 can still have a lane at outX == dstW - 8)
+                    lineSum[v] = make_int4(sum[0], sum[1], sum[2], sum[3]);
+                if (edgeR && laneR)
+                    lineSum[H + v] = make_int4(sum[4], sum[5], sum[6], sum[7]);
+            }
             if (v == H - 1) {  // a band's last, partial trip is flushed after the loop
                 __builtin_amdgcn_wave_barrier();
                 flush_lines(yy - dir * v, H);
@@ -1531,7 +1567,7 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     wait_vmcnt<0>();  // no LDS-DMA may still be writing when the wave (and its LDS) retires
 }
 template <int NY, int NX, int OFFX, int K, int CPW, bool C0ONE, bool LINE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 10 ? 3 : 4))) void lanczos_symb_kernel(LanczosArgs a)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 12 ? 2 : NY > 10 ? 3 : 4))) void lanczos_symb_kernel(LanczosArgs a)
 {
     unsigned bx = blockIdx.x, by = blockIdx.y;
     int rpb = a.rowsPerBand;
@@ -4714,8 +4750,9 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
         np = l.np > 0 ? min(l.np, 62) : (lanes + wpr - 1) / wpr;
         if (np * 8 > l.dstW)
             np = l.dstW / 8;
-        if (l.NY == 12 && (l.dstW + 8 * np - 1) / (8 * np) > 4)
-            np = (lanes + wpr - 1) / wpr;  // (a lane count that needs more than 4 waves: the default)
+        if (l.NY >= 12 && ((l.dstW + 8 * np - 1) / (8 * np) > 4 || (l.NY == 16 && !symb_line(l.dstW, np))))
+            np = (lanes + wpr - 1) / wpr;  // (a lane count that needs more than 4 waves or, Lanczos-5,
+                                           // leaves the line edge scheme: the default)
         opw = 8 * np;
         wpr = (l.dstW + opw - 1) / opw;
     }
@@ -4732,8 +4769,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int lastLanes = (rowNeed - 16 - 1024 * (chunks - 1)) / 16;
     const int cpw = (chunks + wpr - 1) / wpr;
     const bool shared = l.sym == 1 && wpr <= 4 && cpw <= 2;
-    if (l.NY == 12 && !shared)
-        return hipErrorInvalidValue;  // Lanczos-4 2:1: block-shared instantiation only (plan.cpp)
+    if ((l.NY == 12 || l.NY == 16) && !shared)
+        return hipErrorInvalidValue;  // Lanczos-4 / -5 2:1: block-shared instantiation only (plan.cpp)
     // narrow frames: several frames side by side in one 2-wave workgroup (lanczos_stack_kernel)
     const int npf = l.srcW / 16;
     const int fpwMax = npf >= 1 ? std::min(6, 125 / (npf + 1)) : 0;
@@ -4772,7 +4809,9 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
         // block-shared ring (default): one workgroup of wpr waves per row band
         const bool one = (l.cy[0] & 0xffffu) == 1u;
         const bool line = symb_line(l.dstW, np);  // border columns: whole-line scheme
-        ldsBytes = K * 2 * rowPitch + symb_edge_bytes(l.NY) + (cpw * wpr > chunks ? 1024 : 0);
+        if (l.NY == 16 && !line)
+            return hipErrorInvalidValue;  // Lanczos-5: 5 border columns need the line scheme's 8 edge sums
+        ldsBytes = K * 2 * rowPitch + symb_edge_bytes(l.NY, l.NX) + (cpw * wpr > chunks ? 1024 : 0);
         block = 64 * wpr;
 #define IQO_SYMB_L(NY_, NX_, OX_, K_, CPW_, ONE_)                                                       \
     (line ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, CPW_, ONE_, true>)             \
@@ -4788,6 +4827,8 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             kern = IQO_SYMB(10, 12, -5, false);
         else if (l.NY == 12)
             kern = IQO_SYMB(12, 16, -7, false);  // Lanczos-4 2:1 (3 waves per SIMD: the 12-row window)
+        else if (l.NY == 16)
+            kern = IQO_SYMB(16, 20, -9, false);  // Lanczos-5 2:1 (2 waves per SIMD: the 16-row window)
         else
             kern = IQO_SYMB(8, 8, -3, false);
 #undef IQO_SYMB

@@ -191,7 +191,7 @@ struct LanczosDev {
     // symmetric streamer (plan.hpp FastLanczos::sym)
     int sym;                     // 1: block-shared symmetric, 2: per-wave symmetric, 0: accumulator ring
     int NX, offXO;               // unpadded X taps, odd first tap column
-    uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table
+    uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table (Lanczos-5: below)
     int np;                      // producing lanes per wave (0 = auto)
     int xcd;                     // block-shared streamer: XCD-aware workgroup order (speed only)
     int ringPack;                // block-shared streamer: ring rows packed to the bytes they need
@@ -200,6 +200,12 @@ struct LanczosDev {
     int stack;                   // narrow frames: several frames per workgroup (lanczos_stack_kernel)
     int tail;                    // block-shared streamer: short bands for each XCD's last frame
                                  // (0 = auto, -1 = off, n = n bands of that frame)
+    // Lanczos-5 2:1 (NX = 20, block-shared symmetric streamer only) reuses fields that streamer does
+    // not read, so the argument layout of every instantiation stays as it is (growing it cost C2
+    // 1.5 %): X pairs 8, 9 in cy[8], cy[9] (the symmetric streamer reads cy[0 .. NY/2)); the edge
+    // lanes' 8 exact divisions per side (5 border columns: left lane k < 8, right lane k >= 8,
+    // identity in the interior) as multipliers in cx[0 .. 16) (the ring streamer's padded table)
+    // and shifts in xM[0 .. 8), xT[0 .. 8) (the 4-column scheme's constants)
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,

@@ -493,7 +493,12 @@ void pick_fast_lanczos(Plan *p)
     const int64_t maxSum = 32768 * sabs + (1 << 19);
     if (maxSum >= (int64_t(1) << 31) || (maxSum >> 20) >= 32768)
         return;
-    if (p->dstW % 8 || x.mainBegin > 4 || p->dstW - x.mainEnd > 4 || y.mainBegin > 16 || p->dstH - y.mainEnd > 16)
+    // Lanczos-5 2:1 (12 + 4 zero Y taps, 20 X taps from 2x - 9): 5 border columns per side, held
+    // by the block-shared streamer's line scheme with 8 edge outputs per side (xM8), >= 256 outputs
+    const bool l5 = KX == 2 && KY == 2 && f.NY == 16 && (xh - xl) == 20 && off == -9 && p->dstW >= 256 &&
+                    p->dstW <= 4 * 62 * 8 && x.mainBegin <= 8 && p->dstW - x.mainEnd <= 8;
+    if (p->dstW % 8 || (!l5 && (x.mainBegin > 4 || p->dstW - x.mainEnd > 4)) || y.mainBegin > 16 ||
+        p->dstH - y.mainEnd > 16)
         return;
     // negative denominators (a border row / column whose valid taps sum below zero) divide by
     // the magnitude and flip the sign: C truncation is symmetric
@@ -509,6 +514,23 @@ void pick_fast_lanczos(Plan *p)
         if (!magic_y(dn < 0 ? -dn : dn, &f.yBotM[i], &f.yBotS[i]))
             return;
         f.yBotNeg |= dn < 0 ? 1 << i : 0;
+    }
+    bool neg8 = false;  // a negative denominator among the 8-output edge lanes (not instantiated)
+    for (int k = 0; k < 16; ++k) {
+        const int c = k < 8 ? k : p->dstW - 16 + k;  // column of edge-lane value k
+        int64_t D = int64_t(1) << 20;
+        if (k < 8 && c < x.mainBegin)
+            D = f.dXLeft[static_cast<size_t>(c)];
+        else if (k >= 8 && c >= x.mainEnd && c >= 0)
+            D = f.dXRight[static_cast<size_t>(c - x.mainEnd)];
+        neg8 |= D < 0;
+        if (D < 0)
+            D = -D;
+        if ((D != (int64_t(1) << 20) && (maxSum / D >= 32768)) || !magic_x(D, &f.xM8[k], &f.xT8[k])) {
+            if (l5)
+                return;
+            break;
+        }
     }
     for (int k = 0; k < 8; ++k) {
         const int c = k < 4 ? k : p->dstW - 8 + k;  // column of edge-lane value k
@@ -537,6 +559,8 @@ void pick_fast_lanczos(Plan *p)
     // streamer only (no ring-streamer instantiation), so only where that one runs: <= 4 waves of
     // 62 producing lanes per row, symmetric Y taps, no negative denominators
     const bool l4 = KY == 2 && KX == 2 && f.NY == 12 && (xh - xl) == 16 && off == -7 && p->dstW <= 4 * 62 * 8;
+    if (l5 && neg8)
+        return;
     // symmetric variant: (NY, NX, offXO) = (10, 12, -5) Lanczos-3 2:1, (8, 8, -3) Lanczos-2 2:1
     f.NX = xh - xl;
     f.offXO = off;
@@ -544,10 +568,10 @@ void pick_fast_lanczos(Plan *p)
     bool symY = (f.NY % 2) == 0;
     for (int i = 0; symY && i < f.NY / 2; ++i)
         symY = f.cy[static_cast<size_t>(i)] == f.cy[static_cast<size_t>(f.NY - 1 - i)];
-    f.sym = (inst || l4) && symY && (off & 1) && !f.yTopNeg && !f.yBotNeg && !f.xNeg &&
+    f.sym = (inst || l4 || l5) && symY && (off & 1) && !f.yTopNeg && !f.yBotNeg && (!f.xNeg || l5) &&
             ((f.NY == 10 && f.NX == 12 && off == -5) || (f.NY == 8 && f.NX == 8 && off == -3) ||
-             (f.NY == 12 && f.NX == 16 && off == -7));
-    if (l4 && f.sym)
+             (f.NY == 12 && f.NX == 16 && off == -7) || (f.NY == 16 && f.NX == 20 && off == -9));
+    if ((l4 || l5) && f.sym)
         inst = true;
     if (!inst || (p->srcW % 16) || p->srcW > 8192)
         return;

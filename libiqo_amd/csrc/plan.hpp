@@ -72,6 +72,8 @@ struct FastLanczos {
     // D = 2^20, for columns of those lanes that are not border columns).
     uint32_t yTopM[16] = {}, yBotM[16] = {}, xM[8] = {};
     int32_t yTopS[16] = {}, yBotS[16] = {}, xT[8] = {};
+    uint32_t xM8[16] = {};  // the same for the edge lanes' 8 outputs each (Lanczos-5 2:1: 5 border
+    int32_t xT8[16] = {};   //   columns per side; left lane k < 8, right lane k >= 8)
     // bit i: border row / column i divides by a negative denominator (the pxScale-2 chroma tables;
     // accumulator-ring streamer only)
     int yTopNeg = 0, yBotNeg = 0, xNeg = 0;

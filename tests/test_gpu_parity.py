@@ -332,6 +332,9 @@ STREAM_SHAPES = [
     (4, 1936, 1090, 968, 545),
     (4, 640, 480, 320, 240),
     (4, 2064, 40, 1032, 20),
+    (5, 3840, 2160, 1920, 1080),  # Lanczos-5 2:1: 16-row window, 5 border columns per side (8 edge sums)
+    (5, 640, 480, 320, 240),
+    (5, 2064, 40, 1032, 20),
 ]
 
 
@@ -1200,7 +1203,7 @@ RYX_SHAPES = [
     ("lanczos", 1, 1280, 720, 640, 360, 1),      # 2:1 Lanczos-1
     ("lanczos", 4, 4096, 1080, 2048, 540, 1),    # 2:1 Lanczos-4 .. -9: 12 .. 24 row taps (Lanczos-4 wider
                                                  # than the symmetric streamer's 4 waves per row)
-    ("lanczos", 5, 1280, 720, 640, 360, 1),
+    ("lanczos", 5, 4096, 720, 2048, 360, 1),     # (wider than the symmetric streamer's 4 waves)
     ("lanczos", 6, 1280, 720, 639, 360, 1),
     ("lanczos", 7, 720, 480, 360, 240, 1),
     ("lanczos", 8, 1280, 720, 640, 360, 1),
