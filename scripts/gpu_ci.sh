@@ -64,7 +64,7 @@ for l in open('$OUT/bench_lines.jsonl'):
 prof)
   cd /tmp || exit 1
   for c in ${PROF_CFGS:-c2 c3 c4 g1 g2 g3}; do
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o run -- python3 "$ROOT/bench.py" --config $c --steps 10 --warmup 2 --no-cpu --no-verify --no-probe --alt-frames 0 > "$OUT/prof_$c.log" 2>&1 || { echo "prof $c failed"; tail -20 "$OUT/prof_$c.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o run -- python3 "$ROOT/bench.py" --config $c --steps 40 --warmup 5 --no-cpu --no-verify --no-probe --alt-frames 0 > "$OUT/prof_$c.log" 2>&1 || { echo "prof $c failed"; tail -20 "$OUT/prof_$c.log"; exit 1; }
   done
   cd "$ROOT" || exit 1
   ;;
