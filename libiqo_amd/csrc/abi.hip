@@ -58,6 +58,7 @@ struct iqo_hip_plan {
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int tail = 0;           // block-shared streamer: short bands for each XCD's last frame (0 auto, -1 off, n bands)
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
+    int ryxAdj = 1;         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
@@ -580,6 +581,7 @@ void reset_options(iqo_hip_plan *h)
     h->tail = 0;
     h->stack = 1;
     h->ryxSplit = 1;
+    h->ryxAdj = 1;
     h->lanes = 0;
     h->ratioPrefetch = 0;
     h->ratioAlt = 1;
@@ -973,11 +975,22 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     d.parts = 0;
     d.threads = 512;
     const int tw = h->ryxSplit == 2 ? 128 : h->ryxSplit == 3 ? 64 : 256;
-    if (h->ryxSplit >= 2 && split_min(tw))
-        return d;
-    if (!(h->ryxSplit == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
+    if (!(h->ryxSplit >= 2 && split_min(tw)) &&
+        !(h->ryxSplit == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
         !(h->ryxSplit == 1 && split(4, 256)))
         split_min(512);
+    // adjacent column pairs per thread (9:4 only, where every pair's windows start 1 or 2 pairs
+    // apart, i.e. columns at 2:1 or more): one LDS run of NP + 2 dwords for both columns
+    d.adj = 0;
+    if (d.parts > 0 && h->ryxAdj && d.P == 9 && d.Q == 4) {
+        bool ok = true;
+        for (int k = 0; k < d.parts && ok; ++k)
+            for (int x = d.xs[k]; x + 1 < d.xs[k + 1] && ok; x += 2) {
+                const int dl = t.cols[static_cast<size_t>(x + 1) * 4] - t.cols[static_cast<size_t>(x) * 4];
+                ok = dl == 4 || dl == 8;
+            }
+        d.adj = ok ? 1 : 0;
+    }
     return d;
 }
 
@@ -1338,6 +1351,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 3)          // workgroup per row where it fits, 1 default, 2 / 3 parts of 2 / 1 waves
             return IQO_HIP_EINVAL;
         h->ryxSplit = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryx_adj")) {  // ratio-Y kernel adjacent column pairs (speed only): 0 off, 1 where they fit
+        if (value < 0 || value > 1)
+            return IQO_HIP_EINVAL;
+        h->ryxAdj = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stack")) {  // narrow frames side by side in one workgroup (speed only):

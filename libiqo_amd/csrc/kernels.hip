@@ -3362,7 +3362,7 @@ struct RyxArgs {
 #ifndef IQO_RYX_WPE
 #define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
 #endif
-template <bool LZ, int P, int Q, int T, int NP, int PD>
+template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
 {
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
@@ -3422,9 +3422,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // Thread t owns output columns xLo + t and xLo + half + t: neighbouring lanes read windows
     // one output column apart, so the work-row reads spread over the LDS banks (columns 2t, 2t + 1
     // put 4:1 lanes 16 B apart: 8-way bank conflicts, 56 % of the LDS cycles; 9:4 44 %)
-    const int half = (xHi - xLo + 1) >> 1;
-    const int xc[2] = {xLo + t, xLo + half + t};
-    uint32_t cf[2][NP];
+    // ADJ (column ratio >= 2, ryx_dev checks every pair): thread t owns the adjacent columns
+    // xLo + 2t, xLo + 2t + 1, whose windows start 1 or 2 pairs apart: one run of NP + 2 dwords
+    // serves both (10 reads instead of 16 at NP 8), the second column's pairs padded to NP + 1
+    const int half = ADJ ? 1 : (xHi - xLo + 1) >> 1;
+    const int xc[2] = {ADJ ? xLo + 2 * t : xLo + t, ADJ ? xLo + 2 * t + 1 : xLo + half + t};
+    constexpr int NC1 = ADJ ? NP + 1 : NP;  // coefficient pairs of the second column
+    uint32_t cf[2][NC1];
     int aoff[2];
     uint32_t mm[2];
     int sh[2];
@@ -3457,12 +3461,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
         aoffB[k] = rot ? aoff[k] : aoff[k] + 4 * (NP - 1);
         aoff[k] += 4 * rot;
     }
+    if constexpr (ADJ) {
+        const bool two = aoff[1] - aoff[0] == 8;  // else 4 (the pair's last thread past xHi: unused)
+#pragma unroll
+        for (int q = NP; q >= 1; --q)
+            cf[1][q] = two ? cf[1][q - 1] : q < NP ? cf[1][q] : 0u;
+        cf[1][0] = two ? 0u : cf[1][0];
+    }
     // interior Lanczos columns divide by 2^20 (magic_x: m = 2^31, shift 19), which is one
     // saturating pack of both columns; only the few border columns take the exact division
     const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
     // one byte store per column (a wave stores 64 consecutive bytes per instruction)
-    const int stoff = t < half && IQO_RYX_EXP != 2 ? xc[0] : OOB;
-    const int stoff1 = t < half && xc[1] < xHi && IQO_RYX_EXP != 2 ? xc[1] : OOB;
+    const int stoff = (ADJ ? xc[0] < xHi : t < half) && IQO_RYX_EXP != 2 ? xc[0] : OOB;
+    const int stoff1 = (ADJ || t < half) && xc[1] < xHi && IQO_RYX_EXP != 2 ? xc[1] : OOB;
 
     // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1.
     // Rows outside the image load as zero (the reference's masked border sums); rows past the
@@ -3562,13 +3573,22 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
             if (IQO_RYX_EXP != 3)  // experiment 3: no barrier (timing only)
                 __syncthreads();
             const uint8_t *wr = lds + B * pitch;
-            uint32_t w[2][NP];
+            // window pair q of column k: w[k][q] (ADJ: one run, the second column from pair 1)
+            constexpr int NR = ADJ ? NP + 2 : NP;
+            uint32_t w[ADJ ? 1 : 2][NR];
+            if constexpr (ADJ) {
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
+                for (int q = 0; q < NR; ++q)
+                    w[0][q] = reinterpret_cast<const uint32_t *>(wr + aoff[0])[q];
+            } else {
 #pragma unroll
-                for (int q = 0; q < NP; ++q)
-                    w[k][q] = q + 1 < NP ? reinterpret_cast<const uint32_t *>(wr + aoff[k])[q]
-                                         : *reinterpret_cast<const uint32_t *>(wr + aoffB[k]);
+                for (int k = 0; k < 2; ++k)
+#pragma unroll
+                    for (int q = 0; q < NP; ++q)
+                        w[k][q] = q + 1 < NP ? reinterpret_cast<const uint32_t *>(wr + aoff[k])[q]
+                                             : *reinterpret_cast<const uint32_t *>(wr + aoffB[k]);
+            }
+            auto wq = [&](int k, int q) -> uint32_t { return ADJ ? w[0][k + q] : w[k][q]; };
             // the next row's vertical pass (the next trip's first row after the trip's last)
             auto next_vertical = [&]() {
                 const int gn = base + (r + 1) / Q;
@@ -3588,10 +3608,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
                 int acc[2];
 #pragma unroll
                 for (int k = 0; k < 2; ++k) {
-                    acc[k] = sdot2_vv(w[k][0], cf[k][0], 1 << 19);
+                    acc[k] = sdot2_vv(wq(k, 0), cf[k][0], 1 << 19);
 #pragma unroll
-                    for (int q = 1; q < NP; ++q)
-                        acc[k] = sdot2(w[k][q], cf[k][q], acc[k]);
+                    for (int q = 1; q < (k ? NC1 : NP); ++q)
+                        acc[k] = sdot2(wq(k, q), cf[k][q], acc[k]);
                 }
                 if (edgeT) {
                     const uint32_t o0 = min(__umulhi(static_cast<uint32_t>(max(acc[0], 0)), mm[0]) >> sh[0], 255u);
@@ -3606,8 +3626,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
                 for (int k = 0; k < 2; ++k) {
                     uint32_t acc = 1u << 22;
 #pragma unroll
-                    for (int q = 0; q < NP; ++q)
-                        acc = udot2(w[k][q], cf[k][q], acc);
+                    for (int q = 0; q < (k ? NC1 : NP); ++q)
+                        acc = udot2(wq(k, q), cf[k][q], acc);
                     const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
                     o[k] = u > 255 ? 255 : u;
                 }
@@ -4527,28 +4547,34 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     // zero outer taps of every phase), column pairs
     // PD: groups of P source rows loaded ahead (ubench: with one group in flight the source loads
     // cost G5 19 % and Lanczos-4 2:1 27 % of the kernel time -- latency, not bandwidth)
+    // ADJ: adjacent column pairs per thread (9:4 rows with columns >= 2:1, ryx_dev d.adj)
     struct Inst {
         bool lz;
         int P, Q, T, NP;
+        bool adj;
         const void *kern;
     };
-#define IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_)                                                                      \
-    {LZ_, P_, Q_, T_, NP_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_>)}
+#define IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, ADJ_)                                                              \
+    {LZ_, P_, Q_, T_, NP_, ADJ_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_, ADJ_>)}
+#define IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_) IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, false)
+#define IQO_RYX2(LZ_, P_, Q_, T_, NP_, PD_) IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_), IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, true)
     static const Inst kInst[] = {
-        IQO_RYX(true, 9, 4, 12, 8, 2), IQO_RYX(true, 9, 4, 12, 10, 2),  // Lanczos-3 9:4 (1080p -> 480p, -> 640x480)
-        IQO_RYX(true, 9, 4, 8, 6, 2), IQO_RYX(true, 9, 4, 8, 7, 2),     // Lanczos-2 9:4
-        IQO_RYX(false, 9, 4, 4, 3, 2),                                  // Area 9:4
+        IQO_RYX2(true, 9, 4, 12, 8, 2), IQO_RYX2(true, 9, 4, 12, 10, 2),  // Lanczos-3 9:4 (1080p -> 480p, -> 640x480)
+        IQO_RYX2(true, 9, 4, 8, 6, 2), IQO_RYX2(true, 9, 4, 8, 7, 2),     // Lanczos-2 9:4
+        IQO_RYX2(false, 9, 4, 4, 3, 2),                                   // Area 9:4
         IQO_RYX(true, 4, 1, 14, 13, 4), IQO_RYX(true, 4, 1, 14, 9, 4),  // Lanczos-3 / -2 4:1 (4K -> 960x540)
         IQO_RYX(true, 2, 1, 4, 3, 2),                                   // Lanczos-1 2:1
         IQO_RYX(true, 2, 1, 12, 9, 3), IQO_RYX(true, 2, 1, 16, 11, 4),  // Lanczos-4 / -5 2:1
         IQO_RYX(true, 2, 1, 18, 13, 5), IQO_RYX(true, 2, 1, 20, 15, 5), // Lanczos-6 / -7 2:1
         IQO_RYX(true, 2, 1, 22, 17, 2), IQO_RYX(true, 2, 1, 24, 19, 2), // Lanczos-8 / -9 2:1
     };
+#undef IQO_RYX2
 #undef IQO_RYX
+#undef IQO_RYX_A
     const void *kern = nullptr;
     int trip = 0;
     for (const Inst &k : kInst)
-        if (k.lz == d.lanczos && k.P == d.P && k.Q == d.Q && k.T == d.taps && k.NP == d.NP) {
+        if (k.lz == d.lanczos && k.P == d.P && k.Q == d.Q && k.T == d.taps && k.NP == d.NP && k.adj == (d.adj != 0)) {
             kern = k.kern;
             const int span = (k.P * (k.Q - 1)) / k.Q + k.T, nw0 = (span + k.P - 1) / k.P * k.P;
             const int nw = ((nw0 / k.P) * k.Q) % 2 ? nw0 + k.P : nw0;

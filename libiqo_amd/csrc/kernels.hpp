@@ -135,6 +135,9 @@ struct RyxDev {
     int parts;                   // 1 .. 16
     int threads;                 // threads per workgroup (4 source columns each, a multiple of 64)
     int xs[17], cs[16], ce[16];
+    // 1: every thread's two columns are adjacent (xs[k] + 2i, + 1) with windows 1 or 2 pairs apart
+    // (kernels.hip ryx_kernel ADJ); 0: columns i and half + i of the part
+    int adj = 0;
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

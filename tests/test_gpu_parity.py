@@ -1241,6 +1241,10 @@ def test_ryx_matches_oracle(cfg):
         one = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
         one.set_option("ryx_split", split)
         assert (one.resize_tensor(src).cpu().numpy() == out).all(), (cfg, split)
+    # one column per thread pair slot (the default takes adjacent column pairs at 9:4 where they fit)
+    sep = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
+    sep.set_option("ryx_adj", 0)
+    assert (sep.resize_tensor(src).cpu().numpy() == out).all(), (cfg, "ryx_adj 0")
     got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
     cuts = [0, 3, dh // 3 + 1, dh // 2, dh - 5, dh]
     for r0, r1 in zip(cuts[:-1], cuts[1:]):
