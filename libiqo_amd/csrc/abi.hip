@@ -58,7 +58,8 @@ struct iqo_hip_plan {
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int tail = 0;           // block-shared streamer: short bands for each XCD's last frame (0 auto, -1 off, n bands)
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
-    int ryxAdj = 1;         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
+    int ryxAdj = 1;
+    int ryxCpt = 1;         // ratio-Y kernel: 6 output columns per thread at the 4:9 upscales (speed only)         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
@@ -582,6 +583,7 @@ void reset_options(iqo_hip_plan *h)
     h->stack = 1;
     h->ryxSplit = 1;
     h->ryxAdj = 1;
+    h->ryxCpt = 1;
     h->lanes = 0;
     h->ratioPrefetch = 0;
     h->ratioAlt = 1;
@@ -945,7 +947,7 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
             }
             cs[k] = k == 0 ? 0 : std::max(0, lo) & ~3;
             ce[k] = k == n - 1 ? d.srcW : std::min(d.srcW, (hi + 3) & ~3);
-            if (ce[k] - cs[k] > 4 * threads || xs[k + 1] - xs[k] > 2 * threads || (k > 0 && lo < 0) ||
+            if (ce[k] - cs[k] > 4 * threads || xs[k + 1] - xs[k] > d.cpt * threads || (k > 0 && lo < 0) ||
                 (k < n - 1 && hi > d.srcW) || xs[k + 1] <= xs[k])
                 return false;
         }
@@ -974,6 +976,21 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // parts of 2 waves / 1 wave.  parts = 0: no split fits (build_plan then drops the kernel).
     d.parts = 0;
     d.threads = 512;
+    // Lanczos-3 upscales (4:9 rows, 4 pairs): 4 output columns per thread in one workgroup per row
+    // (640 -> 1920 in 480 threads instead of four 256-thread parts of 2 columns per thread: 0.333
+    // vs 0.359 ms; Lanczos-2 with 6 columns per thread was slower, 0.379 vs 0.308 ms,
+    // profiles/r04/ryx_up49.txt)
+    d.cpt = 2;
+    if (d.Q > d.P && d.NP >= 4 && h->ryxCpt) {
+        d.cpt = 4;
+        const int need = std::max((d.srcW + 3) / 4, (d.dstW + d.cpt - 1) / d.cpt);
+        if (need <= 512 && split(1, (need + 63) / 64 * 64))
+            return d;
+        if (split_min(512))
+            return d;
+        d.cpt = 2;
+        d.parts = 0;
+    }
     const int tw = h->ryxSplit == 2 ? 128 : h->ryxSplit == 3 ? 64 : 256;
     if (!(h->ryxSplit >= 2 && split_min(tw)) &&
         !(h->ryxSplit == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
@@ -1357,6 +1374,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 1)
             return IQO_HIP_EINVAL;
         h->ryxAdj = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryx_cpt")) {  // ratio-Y upscales: 0 two output columns per thread, 1 six
+        if (value < 0 || value > 1)
+            return IQO_HIP_EINVAL;
+        h->ryxCpt = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stack")) {  // narrow frames side by side in one workgroup (speed only):

@@ -3362,9 +3362,10 @@ struct RyxArgs {
 #ifndef IQO_RYX_WPE
 #define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
 #endif
-template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ>
+template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ, int CPT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
 {
+    static_assert(CPT % 2 == 0 && (!ADJ || CPT == 2), "output columns per thread: pairs");
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
     constexpr int NW0 = (SPAN + P - 1) / P * P;   // register window rows (whole groups of P) ...
     constexpr int NW = ((NW0 / P) * Q) % 2 ? NW0 + P : NW0;  // ... and an even number of rows per trip
@@ -3425,15 +3426,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // ADJ (column ratio >= 2, ryx_dev checks every pair): thread t owns the adjacent columns
     // xLo + 2t, xLo + 2t + 1, whose windows start 1 or 2 pairs apart: one run of NP + 2 dwords
     // serves both (10 reads instead of 16 at NP 8), the second column's pairs padded to NP + 1
-    const int half = ADJ ? 1 : (xHi - xLo + 1) >> 1;
-    const int xc[2] = {ADJ ? xLo + 2 * t : xLo + t, ADJ ? xLo + 2 * t + 1 : xLo + half + t};
-    constexpr int NC1 = ADJ ? NP + 1 : NP;  // coefficient pairs of the second column
-    uint32_t cf[2][NC1];
-    int aoff[2];
-    uint32_t mm[2];
-    int sh[2];
+    // CPT > 2 (upscales, ryx_dev d.cpt): columns xLo + t + k half, k < CPT
+    const int half = ADJ ? 1 : (xHi - xLo + CPT - 1) / CPT;
+    int xc[CPT];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < CPT; ++k)
+        xc[k] = ADJ ? xLo + 2 * t + k : xLo + k * half + t;
+    constexpr int NC1 = ADJ ? NP + 1 : NP;  // coefficient pairs of the second column
+    uint32_t cf[CPT][NC1];
+    int aoff[CPT];
+    uint32_t mm[CPT];
+    int sh[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k) {
         const int x = min(xc[k], xHi - 1);
         const int4 c = d.cols[x];
         aoff[k] = c.x - 2 * cLo;  // work-row byte offset relative to this part's first column
@@ -3449,9 +3454,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // touches 32 distinct banks.  The coefficient pairs are rotated the same way, once.
     constexpr bool ROT = P == 4 && Q == 1;
     const int rot = ROT ? (t >> 4) & 1 : 0;
-    int aoffB[2];  // byte offset of the last pair read (aoff[k] + 4 rot + 4 q for the others)
+    int aoffB[CPT];  // byte offset of the last pair read (aoff[k] + 4 rot + 4 q for the others)
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < CPT; ++k) {
         if constexpr (ROT) {
             const uint32_t c0 = cf[k][0];
 #pragma unroll
@@ -3470,10 +3475,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     }
     // interior Lanczos columns divide by 2^20 (magic_x: m = 2^31, shift 19), which is one
     // saturating pack of both columns; only the few border columns take the exact division
-    const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
+    bool edgeAny = false;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        edgeAny = edgeAny || mm[k] != 0x80000000u || sh[k] != 19;
+    const bool edgeT = LZ && edgeAny;
     // one byte store per column (a wave stores 64 consecutive bytes per instruction)
-    const int stoff = (ADJ ? xc[0] < xHi : t < half) && IQO_RYX_EXP != 2 ? xc[0] : OOB;
-    const int stoff1 = (ADJ || t < half) && xc[1] < xHi && IQO_RYX_EXP != 2 ? xc[1] : OOB;
+    int stoff[CPT];
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        stoff[k] = (ADJ || t < half) && xc[k] < xHi && IQO_RYX_EXP != 2 ? xc[k] : OOB;
 
     // relative row q = source row rBase + q; group g's window = relative rows P g .. P g + SPAN - 1.
     // Rows outside the image load as zero (the reference's masked border sums); rows past the
@@ -3575,14 +3586,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
             const uint8_t *wr = lds + B * pitch;
             // window pair q of column k: w[k][q] (ADJ: one run, the second column from pair 1)
             constexpr int NR = ADJ ? NP + 2 : NP;
-            uint32_t w[ADJ ? 1 : 2][NR];
+            uint32_t w[ADJ ? 1 : CPT][NR];
             if constexpr (ADJ) {
 #pragma unroll
                 for (int q = 0; q < NR; ++q)
                     w[0][q] = reinterpret_cast<const uint32_t *>(wr + aoff[0])[q];
             } else {
 #pragma unroll
-                for (int k = 0; k < 2; ++k)
+                for (int k = 0; k < CPT; ++k)
 #pragma unroll
                     for (int q = 0; q < NP; ++q)
                         w[k][q] = q + 1 < NP ? reinterpret_cast<const uint32_t *>(wr + aoff[k])[q]
@@ -3603,27 +3614,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
                 next_vertical();
             // horizontal: the thread's two columns
             const int y = Q * (mLo + g) + j;
-            uint32_t packed;
+            uint32_t packed[CPT / 2];  // bytes of columns 2i, 2i + 1 in the low half
             if constexpr (LZ) {
-                int acc[2];
+                int acc[CPT];
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
+                for (int k = 0; k < CPT; ++k) {
                     acc[k] = sdot2_vv(wq(k, 0), cf[k][0], 1 << 19);
 #pragma unroll
                     for (int q = 1; q < (k ? NC1 : NP); ++q)
                         acc[k] = sdot2(wq(k, q), cf[k][q], acc[k]);
                 }
-                if (edgeT) {
-                    const uint32_t o0 = min(__umulhi(static_cast<uint32_t>(max(acc[0], 0)), mm[0]) >> sh[0], 255u);
-                    const uint32_t o1 = min(__umulhi(static_cast<uint32_t>(max(acc[1], 0)), mm[1]) >> sh[1], 255u);
-                    packed = opaque(o0) | (opaque(o1) << 8);
-                } else {
-                    packed = pack_lo(acc[0], acc[1]);  // sat_u8(acc >> 20) of both columns
+#pragma unroll
+                for (int i = 0; i < CPT / 2; ++i) {
+                    if (edgeT) {
+                        const uint32_t o0 =
+                            min(__umulhi(static_cast<uint32_t>(max(acc[2 * i], 0)), mm[2 * i]) >> sh[2 * i], 255u);
+                        const uint32_t o1 =
+                            min(__umulhi(static_cast<uint32_t>(max(acc[2 * i + 1], 0)), mm[2 * i + 1]) >> sh[2 * i + 1], 255u);
+                        packed[i] = opaque(o0) | (opaque(o1) << 8);
+                    } else {
+                        packed[i] = pack_lo(acc[2 * i], acc[2 * i + 1]);  // sat_u8(acc >> 20) of both columns
+                    }
                 }
             } else {
-                int o[2];
+                int o[CPT];
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
+                for (int k = 0; k < CPT; ++k) {
                     uint32_t acc = 1u << 22;
 #pragma unroll
                     for (int q = 0; q < (k ? NC1 : NP); ++q)
@@ -3631,12 +3647,16 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
                     const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
                     o[k] = u > 255 ? 255 : u;
                 }
-                packed = opaque(static_cast<uint32_t>(o[0])) | (opaque(static_cast<uint32_t>(o[1])) << 8);
+#pragma unroll
+                for (int i = 0; i < CPT / 2; ++i)
+                    packed[i] = opaque(static_cast<uint32_t>(o[2 * i])) | (opaque(static_cast<uint32_t>(o[2 * i + 1])) << 8);
             }
             const bool ok = y >= y0 && y < y1;
             const int rowOff = ok ? (y - dstRow0) * dstSt : OOB;
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff + rowOff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed >> 8), dstR, stoff1 + rowOff, 0, 0);
+#pragma unroll
+            for (int k = 0; k < CPT; ++k)
+                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed[k / 2] >> (8 * (k & 1))), dstR,
+                                                     stoff[k] + rowOff, 0, 0);
             if constexpr (!PIPE)
                 next_vertical();
         });
@@ -4548,14 +4568,17 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     // PD: groups of P source rows loaded ahead (ubench: with one group in flight the source loads
     // cost G5 19 % and Lanczos-4 2:1 27 % of the kernel time -- latency, not bandwidth)
     // ADJ: adjacent column pairs per thread (9:4 rows with columns >= 2:1, ryx_dev d.adj)
+    // CPT: output columns per thread (upscales, ryx_dev d.cpt)
     struct Inst {
         bool lz;
         int P, Q, T, NP;
         bool adj;
+        int cpt;
         const void *kern;
     };
-#define IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, ADJ_)                                                              \
-    {LZ_, P_, Q_, T_, NP_, ADJ_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_, ADJ_>)}
+#define IQO_RYX_C(LZ_, P_, Q_, T_, NP_, PD_, ADJ_, CPT_)                                                        \
+    {LZ_, P_, Q_, T_, NP_, ADJ_, CPT_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_, ADJ_, CPT_>)}
+#define IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, ADJ_) IQO_RYX_C(LZ_, P_, Q_, T_, NP_, PD_, ADJ_, 2)
 #define IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_) IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, false)
 #define IQO_RYX2(LZ_, P_, Q_, T_, NP_, PD_) IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_), IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, true)
     static const Inst kInst[] = {
@@ -4567,14 +4590,18 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         IQO_RYX(true, 2, 1, 12, 9, 3), IQO_RYX(true, 2, 1, 16, 11, 4),  // Lanczos-4 / -5 2:1
         IQO_RYX(true, 2, 1, 18, 13, 5), IQO_RYX(true, 2, 1, 20, 15, 5), // Lanczos-6 / -7 2:1
         IQO_RYX(true, 2, 1, 22, 17, 2), IQO_RYX(true, 2, 1, 24, 19, 2), // Lanczos-8 / -9 2:1
+        IQO_RYX(true, 4, 9, 6, 4, 2), IQO_RYX(true, 4, 9, 4, 3, 2),     // Lanczos-3 / -2 4:9 up (480 -> 1080 rows)
+        IQO_RYX_C(true, 4, 9, 6, 4, 2, false, 4),
     };
 #undef IQO_RYX2
 #undef IQO_RYX
 #undef IQO_RYX_A
+#undef IQO_RYX_C
     const void *kern = nullptr;
     int trip = 0;
     for (const Inst &k : kInst)
-        if (k.lz == d.lanczos && k.P == d.P && k.Q == d.Q && k.T == d.taps && k.NP == d.NP && k.adj == (d.adj != 0)) {
+        if (k.lz == d.lanczos && k.P == d.P && k.Q == d.Q && k.T == d.taps && k.NP == d.NP && k.adj == (d.adj != 0) &&
+            k.cpt == d.cpt) {
             kern = k.kern;
             const int span = (k.P * (k.Q - 1)) / k.Q + k.T, nw0 = (span + k.P - 1) / k.P * k.P;
             const int nw = ((nw0 / k.P) * k.Q) % 2 ? nw0 + k.P : nw0;
@@ -4595,12 +4622,12 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
             return hipErrorInvalidValue;
         maxSpan = 0;
         for (int k = 0; k < d.parts; ++k) {
-            if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > 2 * threads || d.cs[k] % 4 ||
+            if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > d.cpt * threads || d.cs[k] % 4 ||
                 d.cs[k] < 0 || d.ce[k] > d.srcW || d.ce[k] - d.cs[k] > 4 * threads || d.ce[k] <= d.cs[k])
                 return hipErrorInvalidValue;
             maxSpan = std::max(maxSpan, d.ce[k] - d.cs[k]);
         }
-    } else if (d.srcW > 4 * threads || d.dstW > 2 * threads) {
+    } else if (d.srcW > 4 * threads || d.dstW > d.cpt * threads) {
         return hipErrorInvalidValue;
     }
     const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);

@@ -138,6 +138,7 @@ struct RyxDev {
     // 1: every thread's two columns are adjacent (xs[k] + 2i, + 1) with windows 1 or 2 pairs apart
     // (kernels.hip ryx_kernel ADJ); 0: columns i and half + i of the part
     int adj = 0;
+    int cpt = 2;                 // output columns per thread (2; 4 at the Lanczos-3 4:9 upscale)
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

@@ -1397,32 +1397,53 @@ void build_ryx(const Plan &p, RyxTables *t)
     if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
         p.srcW < 16 || p.dstH < 4)
         return;
-    // downscales only (the kernel's register window holds the rows of one group of Q outputs)
+    // the kernel's register window holds the rows of one group of Q outputs: downscales, and the
+    // Lanczos 4:9 upscale (480 -> 1080 rows)
     const int64_t g = std::gcd(static_cast<int64_t>(p.srcH), static_cast<int64_t>(p.dstH));
     const int P = static_cast<int>(p.srcH / g), Q = static_cast<int>(p.dstH / g);
     const int T = p.y.taps;
-    if (p.y.phases != Q || P <= Q)
+    if (p.y.phases != Q || Q > 16 || (P <= Q && !(p.method == kLanczos && P == 4 && Q == 9)))
         return;
+    // phase j's reference window starts at P m + floor(P j / Q) + offj[j] for every group m (the
+    // kernel window covers every phase's nonzero taps, so the offsets may differ between phases)
+    std::vector<int> offj(static_cast<size_t>(Q), 0);
+    std::vector<bool> seen(static_cast<size_t>(Q), false);
+    for (int y = 0; y < p.dstH; ++y) {
+        const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
+        const int m = y / Q, j = y % Q;
+        if (ci.kind == kIdentity || ci.tabOff != j * T)
+            return;
+        const int o = ci.srcO - P * m - (P * j) / Q;
+        if (seen[static_cast<size_t>(j)] && offj[static_cast<size_t>(j)] != o)
+            return;
+        seen[static_cast<size_t>(j)] = true;
+        offj[static_cast<size_t>(j)] = o;
+    }
     // Lanczos: outer taps that quantise to zero in every phase are dropped (a zero tap adds
     // nothing to the sum; a masked border row's divisor is the reference's own, magic_y below):
-    // Lanczos-3 9:4 takes 12 of 14 rows, 4:1 14 of 24, Lanczos-4 2:1 12 of 16
-    int trimLo = 0, trimHi = 0;
-    if (p.method == kLanczos) {
-        trimLo = trimHi = T;
-        for (int j = 0; j < Q; ++j) {
-            const int32_t *c = &p.y.table[static_cast<size_t>(j * T)];
-            int lo = 0, hi = 0;
+    // Lanczos-3 9:4 takes 12 of 14 rows, 4:1 14 of 24, Lanczos-4 2:1 12 of 16.  [lowest,
+    // highest]: the rows (relative to P m + floor(P j / Q)) any phase's nonzero taps touch
+    int lowest = 1 << 30, highest = -(1 << 30), maxEnd = -(1 << 30);
+    for (int j = 0; j < Q; ++j) {
+        const int32_t *c = &p.y.table[static_cast<size_t>(j * T)];
+        int lo = 0, hi = T - 1;
+        if (p.method == kLanczos) {
             while (lo < T && c[lo] == 0)
                 ++lo;
-            while (hi < T - lo && c[T - 1 - hi] == 0)
-                ++hi;
-            trimLo = std::min(trimLo, lo);
-            trimHi = std::min(trimHi, hi);
+            while (hi > lo && c[hi] == 0)
+                --hi;
+            if (lo == T)
+                continue;  // an all-zero phase (none in practice)
         }
-        if (trimLo + trimHi >= T)
-            return;
+        lowest = std::min(lowest, offj[static_cast<size_t>(j)] + lo);
+        highest = std::max(highest, offj[static_cast<size_t>(j)] + hi);
+        maxEnd = std::max(maxEnd, offj[static_cast<size_t>(j)] + T);
     }
-    const int TE = T - trimLo - trimHi;
+    if (highest < lowest)
+        return;
+    const int TE = highest - lowest + 1;
+    const int minOff = *std::min_element(offj.begin(), offj.end());  // the kernel window stays inside
+                                                                     // the reference's windows
     // instantiated (method, P, Q, taps, column pairs) shapes: kernels.hip launch_ryx.  The fewest
     // taps >= TE (the window may keep some zero taps), then the fewest pairs that hold every column
     // window (an odd start takes one more entry)
@@ -1433,29 +1454,31 @@ void build_ryx(const Plan &p, RyxTables *t)
                                     {kLanczos, 9, 4, 8, 7},   {kArea, 9, 4, 4, 3},      {kLanczos, 4, 1, 14, 9},
                                     {kLanczos, 4, 1, 14, 13}, {kLanczos, 2, 1, 4, 3},   {kLanczos, 2, 1, 12, 9},
                                     {kLanczos, 2, 1, 16, 11}, {kLanczos, 2, 1, 18, 13}, {kLanczos, 2, 1, 20, 15},
-                                    {kLanczos, 2, 1, 22, 17}, {kLanczos, 2, 1, 24, 19}};
+                                    {kLanczos, 2, 1, 22, 17}, {kLanczos, 2, 1, 24, 19}, {kLanczos, 4, 9, 6, 4},
+                                    {kLanczos, 4, 9, 4, 3}};
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.P == P && S.Q == Q && S.T >= TE && S.T <= T && p.x.taps + 1 <= 2 * S.NP &&
+        if (S.method == p.method && S.P == P && S.Q == Q && S.T >= TE && S.T <= maxEnd - minOff && p.x.taps + 1 <= 2 * S.NP &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))
             best = &S;
     if (!best)
         return;
     const int TK = best->T, NP = best->NP;
-    const int lo = std::min(trimLo, T - TK);  // the kernel window: taps [lo, lo + TK) of every phase
-    const int off = (p.method == kLanczos ? 1 - T / 2 : 0) + lo;
-    // rows: every reference window starts at P m + floor(P j / Q) + (off - lo) and takes phase j
-    for (int y = 0; y < p.dstH; ++y) {
-        const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
-        const int m = y / Q, j = y % Q;
-        if (ci.kind == kIdentity || ci.srcO != P * m + (P * j) / Q + off - lo || ci.tabOff != j * T)
-            return;
-    }
-    t->rowCoef.resize(static_cast<size_t>(Q * TK));
+    // the kernel window of output (m, j): TK rows from P m + floor(P j / Q) + off, ending no later
+    // than the reference's windows (a downscale: taps [lo, lo + TK) of every phase, lo = the
+    // leading zero taps or fewer)
+    const int off = std::min(lowest, maxEnd - TK);
+    t->rowCoef.assign(static_cast<size_t>(Q * TK), 0u);
     for (int j = 0; j < Q; ++j)
-        for (int k = 0; k < TK; ++k) {
-            const uint32_t c = static_cast<uint32_t>(p.y.table[static_cast<size_t>(j * T + lo + k)]) & 0xffffu;
-            t->rowCoef[static_cast<size_t>(j * TK + k)] = c * 0x10001u;
+        for (int k = 0; k < T; ++k) {
+            const int32_t c = p.y.table[static_cast<size_t>(j * T + k)];
+            const int w = offj[static_cast<size_t>(j)] + k - off;  // kernel window row of tap k
+            if (w < 0 || w >= TK) {
+                if (c != 0)
+                    return;
+                continue;
+            }
+            t->rowCoef[static_cast<size_t>(j * TK + w)] = (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u;
         }
     int m0 = 0, m1 = p.dstH;
     if (p.method == kLanczos) {

@@ -52,6 +52,8 @@ SHAPES = [
     ("lanczos", 3, 1280, 720, 3840, 2160),
     ("linear", 0, 1280, 720, 3840, 2160),
     ("lanczos", 3, 640, 480, 1920, 1080),
+    ("lanczos", 2, 640, 480, 1920, 1080),     # 4:9 upscale rows (ryx)
+    ("lanczos", 3, 720, 480, 1620, 1080),
     ("lanczos", 3, 1920, 1080, 1366, 768),
     ("area", 0, 1920, 1080, 1366, 768),
     ("lanczos", 2, 1920, 1080, 1024, 576),

@@ -121,7 +121,8 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 4, 4096, 2160, 2048, 1080, 1), "ryx"),            # (> 4 waves per row) and -5 .. -9 2:1
     (("lanczos", 5, 3840, 2160, 1920, 1080, 1), "lanczos_stream"), # Lanczos-5 2:1: 8 edge sums per side
     (("lanczos", 6, 3840, 2160, 1920, 1080, 1), "ryx"),
-    (("lanczos", 9, 3840, 2160, 1920, 1080, 1), "ryx"),            # (taps beyond the tile tables)
+    (("lanczos", 9, 3840, 2160, 1920, 1080, 1), "ryx"),
+    (("lanczos", 3, 640, 480, 1920, 1080, 1), "ryx"),              # 4:9 upscale rows            # (taps beyond the tile tables)
     (("linear", 0, 3840, 2160, 1920, 1080, 1), "area_int"),        # Linear 2:1: linear_d2 (area kind 8)
 ])
 def test_fast_path_selection(cfg, kernel):

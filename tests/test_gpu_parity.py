@@ -1208,6 +1208,10 @@ RYX_SHAPES = [
     ("lanczos", 7, 720, 480, 360, 240, 1),
     ("lanczos", 8, 1280, 720, 640, 360, 1),
     ("lanczos", 9, 3840, 2160, 1920, 1080, 1),
+    ("lanczos", 3, 640, 480, 1920, 1080, 1),     # 4:9 upscale rows (480 -> 1080), columns 3x
+    ("lanczos", 2, 640, 480, 1920, 1080, 1),
+    ("lanczos", 3, 720, 480, 1620, 1080, 1),     # columns 2.25x
+    ("lanczos", 3, 320, 240, 721, 540, 1),       # odd output width
 ]
 
 
@@ -1245,6 +1249,9 @@ def test_ryx_matches_oracle(cfg):
     sep = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)
     sep.set_option("ryx_adj", 0)
     assert (sep.resize_tensor(src).cpu().numpy() == out).all(), (cfg, "ryx_adj 0")
+    two = libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px)  # Lanczos-3 upscales: 2 instead of 4 columns per thread
+    two.set_option("ryx_cpt", 0)
+    assert (two.resize_tensor(src).cpu().numpy() == out).all(), (cfg, "ryx_cpt 0")
     got = torch.zeros((n, dh, dw), dtype=torch.uint8, device=DEV)
     cuts = [0, 3, dh // 3 + 1, dh // 2, dh - 5, dh]
     for r0, r1 in zip(cuts[:-1], cuts[1:]):

@@ -87,7 +87,10 @@ def _shapes():
            ("ryx", "lanczos", 1, 640, 480, 320, 240), ("ryx", "lanczos", 4, 1920, 1080, 960, 540),   # 2:1
            ("ryx", "lanczos", 5, 640, 360, 320, 180), ("ryx", "lanczos", 6, 640, 360, 320, 180),
            ("ryx", "lanczos", 7, 720, 480, 360, 240), ("ryx", "lanczos", 8, 640, 360, 320, 180),
-           ("ryx", "lanczos", 9, 3840, 2160, 1920, 1080), ("ryx", "lanczos", 9, 5120, 64, 2560, 32)]
+           ("ryx", "lanczos", 9, 3840, 2160, 1920, 1080), ("ryx", "lanczos", 9, 5120, 64, 2560, 32),
+           ("ryx", "lanczos", 3, 640, 480, 1920, 1080), ("ryx", "lanczos", 2, 640, 480, 1920, 1080),  # 4:9 up
+           ("ryx", "lanczos", 3, 720, 480, 1620, 1080), ("ryx", "lanczos", 3, 320, 240, 720, 540),
+           ("ryx", "lanczos", 2, 64, 16, 100, 36)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -103,9 +106,11 @@ def _shapes():
         f = rng.choice((2, 3))
         out.append(("linear_up", "linear", 0, 8 * a, b, f * 8 * a, f * b))
         out.append(("ryx", rng.choice(("lanczos", "area")), 3, sw, 9 * b + 36,
-                    2 * rng.randint(sw // 4 + 1, min(1024, sw) // 2) - rng.randint(0, 1), 4 * b + 16))
+                    2 * rng.randint(sw // 4 + 1, min(1024, sw - 2) // 2) - rng.randint(0, 1), 4 * b + 16))
         out.append(("ryx", "lanczos", rng.choice((1, 4, 5, 6, 7, 8, 9)), sw, 2 * b + 40, sw // 2, b + 20))
         out.append(("ryx", "lanczos", rng.choice((2, 3)), 4 * sw, 4 * b + 40, sw, b + 10))
+        uw = sw // 2 & ~3  # 4:9 rows, columns upscaled (<= 4 coefficient pairs)
+        out.append(("ryx", "lanczos", rng.choice((2, 3)), uw, 4 * b + 16, rng.randint(uw, min(4096, 3 * uw)), 9 * b + 36))
     return out
 
 
