@@ -3411,6 +3411,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
 #endif
     const int span = cHi - cLo;  // this workgroup's source columns [cLo, cHi), 4 per thread
     const int voff = 4 * t < span && IQO_RYX_EXP != 1 ? cLo + 4 * t : OOB;
+    // upscales: waves with no source columns (480 threads over 160 source dwords) skip the
+    // vertical pass and its loads (uniform per wave; not at the downscales, where every wave has
+    // source columns and the branch costs Lanczos-3 4:1 its prefetch: 0.36 -> 0.82 ms)
+    const bool srcWave = Q <= P || 256 * __builtin_amdgcn_readfirstlane(t >> 6) < span;
 
     // work rows: two buffers of (pad + span + pad) u16, zero padding written once
     const int pitch = PADB + 2 * span + PADB;
@@ -3603,7 +3607,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
             // the next row's vertical pass (the next trip's first row after the trip's last)
             auto next_vertical = [&]() {
                 const int gn = base + (r + 1) / Q;
-                if (gn < nG) {
+                if (gn < nG && srcWave) {
                     if constexpr (jn == 0)
                         enter_group(std::integral_constant<int, vn>{}, gn);
                     vertical(std::integral_constant<int, vn>{}, std::integral_constant<int, jn>{},
