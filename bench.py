@@ -265,6 +265,43 @@ def alt_batch(make_step, frames_alt, bytes_per_frame, dev, steps=20, warmup=3):
             "achieved": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4)}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): start N
+    rank processes of this same command line, one per GPU, as torch.distributed.run would (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT), wait for them and return
+    the worst exit status.  This process never touches the GPU (no torch import): the ranks are
+    fresh children, not an exec of an initialised process.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def spawn_probe():
+    """--spawn-probe: the rank plumbing of spawn_ranks without a GPU (CPU test): every rank joins a
+    gloo group, all-reduces its rank, and rank 0 prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(dist.get_rank())])
+    dist.all_reduce(t)
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, {"rank": dist.get_rank(), "local_rank": int(os.environ["LOCAL_RANK"])})
+    if dist.get_rank() == 0:
+        print(json.dumps({"world_size": dist.get_world_size(), "rank_sum": t.item(), "ranks": got}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -286,7 +323,14 @@ def main():
     ap.add_argument("--force-general", action="store_true")
     ap.add_argument("--option", action="append", default=[], metavar="KEY=VALUE",
                     help="plan option (iqo_hip_plan_set_option), repeatable; speed-only A/B knobs")
+    ap.add_argument("--spawn-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if args.spawn_probe:
+        spawn_probe()
+        return
 
     import torch
 
@@ -296,7 +340,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log("warning: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+        log("warning: --gpus %d but WORLD_SIZE %d (launched by torch.distributed.run); using WORLD_SIZE" %
+            (args.gpus, world))
     dist = None
     # IQO_BENCH_DIST=gloo rehearses the N>1 image-shard path with several ranks per GPU (rank r uses
     # device r % device_count, control collectives over gloo); the real multi-GPU run uses RCCL
@@ -407,8 +452,15 @@ def main():
 
     t = torch.tensor([wall, t_sc if args.shard == "band" else 0.0, kern_ms], dtype=torch.float64,
                      device="cpu" if backend == "gloo" else dev)
+    rank_kern = [kern_ms]
+    pg_world = 1
     if dist:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # timing bookkeeping only, not the data path
+        # timing bookkeeping only, not the data path: every rank's kernel ms, then the MAX
+        allk = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allk, t)
+        rank_kern = [float(x[2].item()) for x in allk]
+        pg_world = dist.get_world_size()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
     # the slowest rank's wall time and the slowest rank's kernel time
     wall_max, scatter_max, kern_ms = float(t[0].item()), float(t[1].item()), float(t[2].item())
 
@@ -535,6 +587,12 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if dist:
+            res["ranks"] = {"process_group_world_size": pg_world, "backend": backend,
+                            "kernel_ms_per_launch_min": round(min(rank_kern), 4),
+                            "kernel_ms_per_launch_max": round(max(rank_kern), 4),
+                            "devices": "one GPU per rank" if backend != "gloo" else
+                                       "rank r on device r %% %d (gloo rehearsal)" % torch.cuda.device_count()}
         if band_info:
             res["band"] = band_info
         if alt:

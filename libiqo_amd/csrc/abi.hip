@@ -58,8 +58,8 @@ struct iqo_hip_plan {
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int tail = 0;           // block-shared streamer: short bands for each XCD's last frame (0 auto, -1 off, n bands)
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
-    int ryxAdj = 1;
-    int ryxCpt = 1;         // ratio-Y kernel: 6 output columns per thread at the 4:9 upscales (speed only)         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
+    int ryxAdj = 1;         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
+    int ryxCpt = 1;         // ratio-Y kernel: 4 output columns per thread at the Lanczos 4:9 upscales (speed only)
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
@@ -1082,6 +1082,14 @@ iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
     return g;
 }
 
+// The ratio-Y kernel is usable when its tables exist and a column split fits for the plan's
+// CURRENT options (ryx_split / ryx_cpt are speed options; upload_exact checked the defaults only).
+// The defaults end in split_min(512), the widest split, so when they fit every option does.
+bool ryx_usable(const iqo_hip_plan *h)
+{
+    return h->ryx.ok && h->useRyx && ryx_dev(h).parts > 0;
+}
+
 // The kernel family a full-frame call with aligned pointers and strides runs.
 int plan_kernel(const iqo_hip_plan *h)
 {
@@ -1098,7 +1106,7 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_LANCZOS_D31;
     // (ryx also takes shapes whose taps exceed the tile kernel's tables: Lanczos-8/9 2:1)
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE || (k == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
-        h->ryx.ok && h->useRyx)
+        ryx_usable(h))
         k = IQO_KERNEL_RYX;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->at.ok && h->useA32)
         k = IQO_KERNEL_AREA_D32;
@@ -1147,7 +1155,7 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     // exact vertical ratio, tabled columns: dword loads; 2-byte stores (1-byte stores when the
     // destination is not 2-byte aligned, launch_ryx)
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE || (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
-        h->ryx.ok && h->useRyx && aligned(src, 4, srcSt, srcFrameSt))
+        aligned(src, 4, srcSt, srcFrameSt) && ryx_usable(h))
         kernel = IQO_KERNEL_RYX;
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
@@ -1264,6 +1272,13 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_l23(l23_dev(h), io, rb, re, h->bands, s);
         else
             e = iqo_amd::launch_general(general_dev(h), io, rb, re, s);
+        // the launchers reject a parameter set they have no instantiation for before launching
+        // (hipErrorInvalidValue / hipErrorNotSupported): a plan / kernel mismatch, reported as such
+        // (the drop-in classes report those on every call instead of falling back for good)
+        if (e == hipErrorInvalidValue)
+            return IQO_HIP_EINVAL;
+        if (e == hipErrorNotSupported)
+            return IQO_HIP_EUNSUP;
         if (e != hipSuccess)
             return IQO_HIP_EHIP;
     }
@@ -1376,7 +1391,8 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->ryxAdj = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "ryx_cpt")) {  // ratio-Y upscales: 0 two output columns per thread, 1 six
+    if (!std::strcmp(key, "ryx_cpt")) {  // ratio-Y upscales: 0 two output columns per thread, 1 four
+                                          // at the Lanczos 4:9 upscales
         if (value < 0 || value > 1)
             return IQO_HIP_EINVAL;
         h->ryxCpt = static_cast<int>(value);

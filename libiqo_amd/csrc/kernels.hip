@@ -887,11 +887,26 @@ constexpr int symb_edge_bytes(int NY, int NX)
                ? 2 * (NY / 2) * (128 + (NX > 16 ? 32 : 16))
                : 2 * IQO_SYMB_EDGE_BATCH * 16;
 }
+// cache policy of dma_row_nt (variant builds, IQO_SYMB_LDPOL): 0 nt, 1 sc0, 2 sc1, 3 sc0 sc1, 4 sc1 nt
+#ifndef IQO_SYMB_LDPOL
+#define IQO_SYMB_LDPOL 0
+#endif
+#if IQO_SYMB_LDPOL == 1
+#define IQO_SYMB_LDPOL_S "sc0"
+#elif IQO_SYMB_LDPOL == 2
+#define IQO_SYMB_LDPOL_S "sc1"
+#elif IQO_SYMB_LDPOL == 3
+#define IQO_SYMB_LDPOL_S "sc0 sc1"
+#elif IQO_SYMB_LDPOL == 4
+#define IQO_SYMB_LDPOL_S "sc1 nt"
+#else
+#define IQO_SYMB_LDPOL_S "nt"
+#endif
 __device__ __forceinline__ void dma_row_nt(uint32_t lds, int voff, __amdgpu_buffer_rsrc_t rsrc, int soff)
 {
     uint32_t keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                 "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+                 "buffer_load_dwordx4 %2, %3, %4 offen " IQO_SYMB_LDPOL_S " lds\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "s"(lds), "v"(voff), "s"(rsrc), "s"(soff)
                  : "memory");
@@ -1234,7 +1249,11 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
     const int dbg = IQO_DBG(a);
     const int svoff = (dbg & 2) ? 0x7ff00000 : voff;
     const int stoff = (produce && !(dbg & 1) && !regL && !regR) ? outX : 0x7ff00000;
+#ifdef IQO_SYMB_STAUX
+    constexpr int STNT = IQO_SYMB_STAUX;  // variant builds: store cache policy bits (1 sc0, 2 nt, 16 sc1)
+#else
     constexpr int STNT = (IQO_SYMB_NT & 2) ? 2 : 0;  // store cache policy (aux: nt)
+#endif
     // Odd bands walk bottom-up: a band boundary's halo rows are then read by both bands at the
     // same time (both at their start or both at their end) and the second read hits the
     // Infinity Cache instead of HBM.  The window arithmetic is symmetric, so only the row order
@@ -4869,6 +4888,11 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
         if (l.NY == 16 && !line)
             return hipErrorInvalidValue;  // Lanczos-5: 5 border columns need the line scheme's 8 edge sums
         ldsBytes = K * 2 * rowPitch + symb_edge_bytes(l.NY, l.NX) + (cpw * wpr > chunks ? 1024 : 0);
+#ifdef IQO_EXP_WGCU  // experiment builds: fewer workgroups per CU by inflating the LDS allocation
+        if (const char *ev = getenv("IQO_EXP_WGCU"))
+            if (atoi(ev) > 0)
+                ldsBytes = std::max(ldsBytes, 163840 / atoi(ev) - 256);
+#endif
         block = 64 * wpr;
 #define IQO_SYMB_L(NY_, NX_, OX_, K_, CPW_, ONE_)                                                       \
     (line ? reinterpret_cast<const void *>(lanczos_symb_kernel<NY_, NX_, OX_, K_, CPW_, ONE_, true>)             \

@@ -135,3 +135,37 @@ def test_oracle_matches_reference_random():
         a = ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)
         b = ol.run_ref(m, d, sw, sh, dw, dh, 1, src, strict=True)
         assert (a == b).all(), (m, d, sw, sh, dw, dh)
+
+
+@pytest.mark.skipif(not ol.ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+def test_oracle_matches_reference_linear_and_ratio_families():
+    """Direct differential for what the sweep above never draws ("Next round" item 1):
+    Linear at random ratios (downscales included; shapes the reference's sanitizer build rejects --
+    Linear upsampling past 2x reads row/column -1 -- are skipped) and the exact-ratio families of
+    the round-4 kernels (2:1 at Lanczos-1..9, 3:1, 4:1, 3x, 4:9 and 9:4 rows), noise input."""
+    import random
+    rng = random.Random(5150)
+    shapes = []
+    for _ in range(60):
+        sw, sh = rng.randint(2, 260), rng.randint(2, 200)
+        dw = rng.randint(max(1, sw // 7), 2 * sw)
+        dh = rng.randint(max(1, sh // 7), 2 * sh)
+        shapes.append(("linear", 0, sw, sh, dw, dh))
+    for d in range(1, 10):
+        shapes.append(("lanczos", d, 16 * rng.randint(2, 20), 2 * rng.randint(8, 40), 0, 0))
+    shapes += [("lanczos", 2, 384, 216, 128, 72), ("lanczos", 3, 300, 150, 100, 50), ("lanczos", 2, 384, 256, 96, 64),
+               ("lanczos", 3, 256, 96, 64, 24), ("lanczos", 2, 128, 40, 384, 120), ("lanczos", 3, 96, 24, 288, 72),
+               ("lanczos", 3, 160, 48, 480, 108), ("lanczos", 2, 200, 36, 450, 81), ("lanczos", 3, 240, 72, 112, 32),
+               ("linear", 0, 3840, 216, 1920, 108), ("linear", 0, 1917, 107, 1280, 72), ("linear", 0, 1000, 70, 333, 25)]
+    n = 0
+    for i, (m, d, sw, sh, dw, dh) in enumerate(shapes):
+        if dw == 0:  # 2:1 at degree d
+            dw, dh = sw // 2, sh // 2
+        if not _ref_clean(m, d, sw, sh, dw, dh):
+            continue
+        src = ol.gen("noise", sw, sh, 700 + i)
+        a = ol.run_oracle(m, d, sw, sh, dw, dh, 1, src)
+        b = ol.run_ref(m, d, sw, sh, dw, dh, 1, src, strict=True)
+        assert (a == b).all(), (m, d, sw, sh, dw, dh)
+        n += 1
+    assert n >= 50

@@ -185,3 +185,24 @@ def test_gather_ops_uneven_bands_and_padded_root(world, dh, root_pad):
             assert op.dst + (op.count - 1) * op.dst_st + op.nbytes <= out.size
     assert (out[:, :, :dw] == ref).all()
     assert (out[:, :, dw:] == 0).all()  # padding never written
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_spawns_one_rank_per_gpu(n):
+    """`python bench.py --gpus N` without a launcher starts N rank processes itself (RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 per rank, bench.spawn_ranks) -- the path the
+    driver's multi-GPU command takes when it does not go through torch.distributed.run.  The hidden
+    --spawn-probe mode runs the same spawn and rendezvous with a gloo group and no GPU."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--spawn-probe"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["world_size"] == n and d["rank_sum"] == n * (n - 1) / 2
+    assert sorted(x["local_rank"] for x in d["ranks"]) == list(range(n))
