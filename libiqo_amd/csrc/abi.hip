@@ -136,14 +136,15 @@ private:
 // reference benchmark constructs one per call, benchmark.cpp:215-226), and one staging set is
 // borrowed per call, so distinct plans can run concurrently from different threads.  The pool
 // is never torn down (the HIP runtime may already be gone at static destruction).
-constexpr int kHostBands = 8;      // output-row bands of the host-pointer pipeline
+constexpr int kHostBands = 8;      // output-row bands of one plane in the host-pointer pipeline
 constexpr int kHostBandRows = 64;  // ... each at least this tall
+constexpr int kHostChunks = 16;    // (plane, band) chunks of one call: events per staging set
 constexpr size_t kHostPipeMinBytes = size_t(4) << 20;  // smaller frames: one band (API latency dominates)
 
 struct HostStage {
     int device = 0;
-    hipStream_t sIn = nullptr, sK = nullptr, sOut = nullptr;
-    hipEvent_t evIn[kHostBands] = {}, evK[kHostBands] = {}, evOut[kHostBands] = {};
+    hipStream_t sIn = nullptr, sK = nullptr, sOut = nullptr, sIn2 = nullptr;
+    hipEvent_t evIn[kHostChunks] = {}, evK[kHostChunks] = {}, evOut[kHostChunks] = {};
     uint8_t *dSrc = nullptr, *dDst = nullptr, *hSrc = nullptr, *hDst = nullptr;
     size_t dSrcCap = 0, dDstCap = 0, hSrcCap = 0, hDstCap = 0;
 };
@@ -153,7 +154,7 @@ std::vector<HostStage *> g_stagePool;
 
 void destroy_stage(HostStage *st)
 {
-    for (int b = 0; b < kHostBands; ++b) {
+    for (int b = 0; b < kHostChunks; ++b) {
         if (st->evIn[b])
             (void)hipEventDestroy(st->evIn[b]);
         if (st->evK[b])
@@ -167,6 +168,8 @@ void destroy_stage(HostStage *st)
         (void)hipStreamDestroy(st->sK);
     if (st->sOut)
         (void)hipStreamDestroy(st->sOut);
+    if (st->sIn2)
+        (void)hipStreamDestroy(st->sIn2);
     (void)hipFree(st->dSrc);
     (void)hipFree(st->dDst);
     (void)hipHostFree(st->hSrc);
@@ -191,8 +194,9 @@ HostStage *acquire_stage(int device)
     st->device = device;
     bool ok = hipStreamCreateWithFlags(&st->sIn, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&st->sK, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&st->sOut, hipStreamNonBlocking) == hipSuccess;
-    for (int b = 0; ok && b < kHostBands; ++b)
+              hipStreamCreateWithFlags(&st->sOut, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&st->sIn2, hipStreamNonBlocking) == hipSuccess;
+    for (int b = 0; ok && b < kHostChunks; ++b)
         ok = hipEventCreateWithFlags(&st->evIn[b], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&st->evK[b], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&st->evOut[b], hipEventDisableTiming) == hipSuccess;
@@ -261,6 +265,13 @@ void copy_rows(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, siz
 // over a small process-wide thread pool: one thread's memcpy (~10 GB/s) is slower than the PCIe
 // link the staged rows then cross.  Created on first use and never torn down (as the staging
 // pool); one parallel copy at a time -- a caller that finds the pool busy copies alone.
+struct RowCopy {
+    uint8_t *dst;
+    size_t dstSt;
+    const uint8_t *src;
+    size_t srcSt, w, rows;
+};
+
 class CopyPool {
 public:
     static CopyPool &instance()
@@ -268,15 +279,28 @@ public:
         static CopyPool *p = new CopyPool();
         return *p;
     }
-    void copy(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, size_t w, size_t rows)
+    // up to kMaxJobs row copies (e.g. the three I420 planes) as ONE parallel job: the rows of all
+    // of them are split evenly over the workers, so a call pays one wake-up, not one per plane
+    static constexpr int kMaxJobs = 3;
+    void copy(const RowCopy *jobs, int n)
     {
+        size_t bytes = 0, rows = 0;
+        for (int j = 0; j < n; ++j) {
+            bytes += jobs[j].w * jobs[j].rows;
+            rows += jobs[j].rows;
+        }
         std::unique_lock<std::mutex> use(useMu_, std::try_to_lock);
-        if (!use.owns_lock() || workers_.empty() || w * rows < (size_t(1) << 20) || rows < 32) {
-            copy_rows(dst, dstSt, src, srcSt, w, rows);
+        // below ~256 KiB one thread's memcpy beats the wake-up of the pool
+        if (!use.owns_lock() || workers_.empty() || n > kMaxJobs || bytes < (size_t(256) << 10) || rows < 32) {
+            for (int j = 0; j < n; ++j)
+                copy_rows(jobs[j].dst, jobs[j].dstSt, jobs[j].src, jobs[j].srcSt, jobs[j].w, jobs[j].rows);
             return;
         }
         std::unique_lock<std::mutex> g(mu_);
-        job_ = Job{dst, dstSt, src, srcSt, w, rows};
+        nJobs_ = n;
+        totalRows_ = rows;
+        for (int j = 0; j < n; ++j)
+            jobs_[j] = jobs[j];
         parts_ = static_cast<int>(workers_.size()) + 1;
         next_ = 0;
         remaining_ = parts_;
@@ -293,12 +317,6 @@ public:
     }
 
 private:
-    struct Job {
-        uint8_t *dst;
-        size_t dstSt;
-        const uint8_t *src;
-        size_t srcSt, w, rows;
-    };
     CopyPool()
     {
         const unsigned hw = std::thread::hardware_concurrency();
@@ -308,11 +326,21 @@ private:
         for (auto &t : workers_)
             t.detach();
     }
+    // part k copies global rows [R k / parts, R (k+1) / parts) of the jobs' rows laid end to end
     void run_part(int part) const
     {
-        const size_t r0 = job_.rows * static_cast<size_t>(part) / static_cast<size_t>(parts_);
-        const size_t r1 = job_.rows * static_cast<size_t>(part + 1) / static_cast<size_t>(parts_);
-        copy_rows(job_.dst + r0 * job_.dstSt, job_.dstSt, job_.src + r0 * job_.srcSt, job_.srcSt, job_.w, r1 - r0);
+        size_t r0 = totalRows_ * static_cast<size_t>(part) / static_cast<size_t>(parts_);
+        const size_t r1 = totalRows_ * static_cast<size_t>(part + 1) / static_cast<size_t>(parts_);
+        size_t base = 0;
+        for (int j = 0; j < nJobs_ && r0 < r1; ++j) {
+            const RowCopy &c = jobs_[j];
+            const size_t a = std::max(r0, base), b = std::min(r1, base + c.rows);
+            if (a < b) {
+                copy_rows(c.dst + (a - base) * c.dstSt, c.dstSt, c.src + (a - base) * c.srcSt, c.srcSt, c.w, b - a);
+                r0 = b;
+            }
+            base += c.rows;
+        }
     }
     void work()
     {
@@ -334,15 +362,20 @@ private:
     std::mutex useMu_, mu_;
     std::condition_variable cv_, done_;
     std::vector<std::thread> workers_;
-    Job job_{};
+    RowCopy jobs_[kMaxJobs]{};
+    int nJobs_ = 0;
+    size_t totalRows_ = 0;
     int parts_ = 0, next_ = 0, remaining_ = 0;
     unsigned long gen_ = 0;
 };
 
 void copy_rows_par(uint8_t *dst, size_t dstSt, const uint8_t *src, size_t srcSt, size_t w, size_t rows)
 {
-    CopyPool::instance().copy(dst, dstSt, src, srcSt, w, rows);
+    const RowCopy c{dst, dstSt, src, srcSt, w, rows};
+    CopyPool::instance().copy(&c, 1);
 }
+
+void copy_planes_par(const RowCopy *jobs, int n) { CopyPool::instance().copy(jobs, n); }
 
 bool is_gfx950(int dev)
 {
@@ -1548,6 +1581,103 @@ int iqo_hip_resize_band(iqo_hip_plan *h, size_t nFrames, size_t dstRow0, size_t 
 // the H2D of band b+1, the kernel of band b and the D2H of band b-1 overlap (PCIe is full
 // duplex).  Pinned host buffers are DMA'd in place; pageable ones are staged through pinned
 // memory by the calling thread one band ahead of the copy engines.
+// One plane of a host-pointer call: the user's buffers and the plane's place in the staging set
+// (device and pinned staging at byte offsets sOff / dOff, row pitches sPitch / dPitch; pinSrc /
+// pinDst: the user buffer is pinned and DMA'd in place).
+struct HostPlane {
+    iqo_hip_plan *h;
+    size_t srcSt;
+    const uint8_t *src;
+    size_t dstSt;
+    uint8_t *dst;
+    size_t sOff, dOff, sPitch, dPitch;
+    bool pinSrc, pinDst;
+};
+
+// The host-pointer pipeline over one or more planes (the I420 planes of one call share it): each
+// plane is cut into output-row bands, and chunk c = (plane, band) goes through
+//   stage its new source rows into pinned memory (the copy pool) -> H2D (two upload streams,
+//   alternating chunks: two SDMA queues) -> the plane's kernel on its band (sK, after the chunk's
+//   uploads) -> D2H of the band (sOut) -> unstage into the user's rows,
+// so the host staging of chunk c + 1 overlaps the upload of chunk c, and every plane's transfers
+// overlap the other planes' instead of each plane paying a synchronous round trip.
+int host_pipeline(HostStage *st, HostPlane *planes, int nPlanes)
+{
+    struct Chunk {
+        int plane, r0, r1;
+    };
+    Chunk ch[kHostChunks];
+    int nc = 0;
+    for (int q = 0; q < nPlanes; ++q) {
+        const int dstH = planes[q].h->p.dstH;
+        const int maxBands = nPlanes == 1 ? kHostBands : q == 0 ? kHostBands / 2 : kHostBands / 4;
+        const int bands = std::max(1, std::min(maxBands, dstH / kHostBandRows));
+        for (int b = 0; b < bands && nc < kHostChunks; ++b)
+            ch[nc++] = Chunk{q, static_cast<int>(static_cast<int64_t>(dstH) * b / bands),
+                             static_cast<int>(static_cast<int64_t>(dstH) * (b + 1) / bands)};
+    }
+    int rowsUp[4] = {0, 0, 0, 0};  // per plane: source rows [0, rowsUp) are queued for upload
+    int lastUp[4] = {-1, -1, -1, -1};  // per plane: the chunk that queued the latest upload
+    for (int c = 0; c < nc; ++c) {
+        HostPlane &P = planes[ch[c].plane];
+        const Plan &p = P.h->p;
+        const size_t W = static_cast<size_t>(p.srcW), w = static_cast<size_t>(p.dstW);
+        int s0, s1;
+        iqo_amd::band_src_rows(p, ch[c].r0, ch[c].r1, &s0, &s1);
+        const bool lastOfPlane = c == nc - 1 || ch[c + 1].plane != ch[c].plane;
+        if (lastOfPlane)
+            s1 = p.srcH;
+        int &up = rowsUp[ch[c].plane];
+        const int prevUp = lastUp[ch[c].plane];
+        hipStream_t sUp = (c & 1) ? st->sIn2 : st->sIn;
+        if (s1 > up) {
+            const size_t n = static_cast<size_t>(s1 - up);
+            const uint8_t *from = P.src + static_cast<size_t>(up) * P.srcSt;
+            size_t fromSt = P.srcSt;
+            if (!P.pinSrc) {
+                uint8_t *pin = st->hSrc + P.sOff + static_cast<size_t>(up) * P.sPitch;
+                copy_rows_par(pin, P.sPitch, from, P.srcSt, W, n);
+                from = pin;
+                fromSt = P.sPitch;
+            }
+            if (hipMemcpy2DAsync(st->dSrc + P.sOff + static_cast<size_t>(up) * P.sPitch, P.sPitch, from, fromSt, W, n,
+                                 hipMemcpyHostToDevice, sUp) != hipSuccess)
+                return IQO_HIP_EHIP;
+            up = s1;
+            lastUp[ch[c].plane] = c;
+        }
+        // the band's rows: this chunk's upload, and the halo rows the plane's previous upload brought
+        if (hipEventRecord(st->evIn[c], sUp) != hipSuccess || hipStreamWaitEvent(st->sK, st->evIn[c], 0) != hipSuccess ||
+            (prevUp >= 0 && prevUp != c && hipStreamWaitEvent(st->sK, st->evIn[prevUp], 0) != hipSuccess))
+            return IQO_HIP_EHIP;
+        const size_t rows = static_cast<size_t>(ch[c].r1 - ch[c].r0);
+        const size_t sBytes = P.sPitch * static_cast<size_t>(p.srcH), dBytes = P.dPitch * static_cast<size_t>(p.dstH);
+        int rc = run_band(P.h, 1, static_cast<size_t>(ch[c].r0), rows, 0, P.sPitch, sBytes, st->dSrc + P.sOff, P.dPitch,
+                          dBytes, st->dDst + P.dOff + static_cast<size_t>(ch[c].r0) * P.dPitch, st->sK);
+        if (rc)
+            return rc;
+        if (hipEventRecord(st->evK[c], st->sK) != hipSuccess || hipStreamWaitEvent(st->sOut, st->evK[c], 0) != hipSuccess)
+            return IQO_HIP_EHIP;
+        uint8_t *to = P.pinDst ? P.dst + static_cast<size_t>(ch[c].r0) * P.dstSt
+                               : st->hDst + P.dOff + static_cast<size_t>(ch[c].r0) * P.dPitch;
+        if (hipMemcpy2DAsync(to, P.pinDst ? P.dstSt : P.dPitch, st->dDst + P.dOff + static_cast<size_t>(ch[c].r0) * P.dPitch,
+                             P.dPitch, w, rows, hipMemcpyDeviceToHost, st->sOut) != hipSuccess ||
+            hipEventRecord(st->evOut[c], st->sOut) != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
+    // output bands leave the pinned staging as they land
+    for (int c = 0; c < nc; ++c) {
+        if (hipEventSynchronize(st->evOut[c]) != hipSuccess)
+            return IQO_HIP_EHIP;
+        const HostPlane &P = planes[ch[c].plane];
+        if (!P.pinDst)
+            copy_rows_par(P.dst + static_cast<size_t>(ch[c].r0) * P.dstSt, P.dstSt,
+                          st->hDst + P.dOff + static_cast<size_t>(ch[c].r0) * P.dPitch, P.dPitch,
+                          static_cast<size_t>(P.h->p.dstW), static_cast<size_t>(ch[c].r1 - ch[c].r0));
+    }
+    return IQO_HIP_OK;
+}
+
 static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
 {
     const Plan &p = h->p;
@@ -1572,7 +1702,7 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
         const uint8_t *from = src;
         size_t fromSt = srcSt;
         if (!pinSrc) {
-            copy_rows(st->hSrc, sPitch, src, srcSt, W, static_cast<size_t>(p.srcH));
+            copy_rows_par(st->hSrc, sPitch, src, srcSt, W, static_cast<size_t>(p.srcH));
             from = st->hSrc;
             fromSt = sPitch;
         }
@@ -1589,59 +1719,11 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
             hipStreamSynchronize(st->sK) != hipSuccess)
             return IQO_HIP_EHIP;
         if (!pinDst)
-            copy_rows(dst, dstSt, st->hDst, dPitch, w, static_cast<size_t>(dstH));
+            copy_rows_par(dst, dstSt, st->hDst, dPitch, w, static_cast<size_t>(dstH));
         return IQO_HIP_OK;
     }
-    const int bands = std::max(1, std::min(kHostBands, dstH / kHostBandRows));
-    auto bandRow = [&](int b) { return static_cast<int>(static_cast<int64_t>(dstH) * b / bands); };
-    int rowsUp = 0;  // source rows [0, rowsUp) are queued for upload
-    for (int b = 0; b < bands; ++b) {
-        const int r0 = bandRow(b), r1 = bandRow(b + 1);
-        int s0, s1;
-        iqo_amd::band_src_rows(p, r0, r1, &s0, &s1);
-        if (b == bands - 1)
-            s1 = p.srcH;
-        if (s1 > rowsUp) {
-            const size_t n = static_cast<size_t>(s1 - rowsUp);
-            const uint8_t *from = src + static_cast<size_t>(rowsUp) * srcSt;
-            size_t fromSt = srcSt;
-            if (!pinSrc) {
-                uint8_t *pin = st->hSrc + static_cast<size_t>(rowsUp) * sPitch;
-                copy_rows_par(pin, sPitch, from, srcSt, W, n);
-                from = pin;
-                fromSt = sPitch;
-            }
-            if (hipMemcpy2DAsync(st->dSrc + static_cast<size_t>(rowsUp) * sPitch, sPitch, from, fromSt, W, n,
-                                 hipMemcpyHostToDevice, st->sIn) != hipSuccess)
-                return IQO_HIP_EHIP;
-            rowsUp = s1;
-        }
-        if (hipEventRecord(st->evIn[b], st->sIn) != hipSuccess || hipStreamWaitEvent(st->sK, st->evIn[b], 0) != hipSuccess)
-            return IQO_HIP_EHIP;
-        const size_t rows = static_cast<size_t>(r1 - r0);
-        int rc = run_band(h, 1, static_cast<size_t>(r0), rows, 0, sPitch, sBytes, st->dSrc, dPitch, dBytes,
-                          st->dDst + static_cast<size_t>(r0) * dPitch, st->sK);
-        if (rc)
-            return rc;
-        if (hipEventRecord(st->evK[b], st->sK) != hipSuccess || hipStreamWaitEvent(st->sOut, st->evK[b], 0) != hipSuccess)
-            return IQO_HIP_EHIP;
-        uint8_t *to = pinDst ? dst + static_cast<size_t>(r0) * dstSt : st->hDst + static_cast<size_t>(r0) * dPitch;
-        if (hipMemcpy2DAsync(to, pinDst ? dstSt : dPitch, st->dDst + static_cast<size_t>(r0) * dPitch, dPitch, w, rows,
-                             hipMemcpyDeviceToHost, st->sOut) != hipSuccess ||
-            hipEventRecord(st->evOut[b], st->sOut) != hipSuccess)
-            return IQO_HIP_EHIP;
-    }
-    // output bands leave the pinned staging as they land
-    for (int b = 0; b < bands; ++b) {
-        if (hipEventSynchronize(st->evOut[b]) != hipSuccess)
-            return IQO_HIP_EHIP;
-        if (!pinDst) {
-            const int r0 = bandRow(b), r1 = bandRow(b + 1);
-            copy_rows_par(dst + static_cast<size_t>(r0) * dstSt, dstSt, st->hDst + static_cast<size_t>(r0) * dPitch, dPitch,
-                      w, static_cast<size_t>(r1 - r0));
-        }
-    }
-    return IQO_HIP_OK;
+    HostPlane pl{h, srcSt, src, dstSt, dst, 0, 0, sPitch, dPitch, pinSrc, pinDst};
+    return host_pipeline(st, &pl, 1);
 }
 
 int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
@@ -1661,6 +1743,7 @@ int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dst
     if (rc) {
         // leave nothing in flight on the staging set before it goes back to the pool
         (void)hipStreamSynchronize(st->sIn);
+        (void)hipStreamSynchronize(st->sIn2);
         (void)hipStreamSynchronize(st->sK);
         (void)hipStreamSynchronize(st->sOut);
     }
@@ -1819,9 +1902,9 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
                 grow_pinned(&st->hSrc, &st->hSrcCap, sBytes) || grow_pinned(&st->hDst, &st->hDstCap, dBytes))
                 rc = IQO_HIP_ENOMEM;
             if (!rc) {
-                copy_rows(st->hSrc, sY, srcY, srcStY, W, H);
-                copy_rows(st->hSrc + oU, sC, srcU, srcStUV, Wc, Hc);
-                copy_rows(st->hSrc + oV, sC, srcV, srcStUV, Wc, Hc);
+                const RowCopy in[3] = {{st->hSrc, sY, srcY, srcStY, W, H}, {st->hSrc + oU, sC, srcU, srcStUV, Wc, Hc},
+                                       {st->hSrc + oV, sC, srcV, srcStUV, Wc, Hc}};
+                copy_planes_par(in, 3);
                 if (hipMemcpyAsync(st->dSrc, st->hSrc, sBytes, hipMemcpyHostToDevice, st->sK) != hipSuccess)
                     rc = IQO_HIP_EHIP;
             }
@@ -1832,9 +1915,9 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
                         hipStreamSynchronize(st->sK) != hipSuccess))
                 rc = IQO_HIP_EHIP;
             if (!rc) {
-                copy_rows(dstY, dstStY, st->hDst, dY, w, hh);
-                copy_rows(dstU, dstStUV, st->hDst + ou, dC, wc, hc);
-                copy_rows(dstV, dstStUV, st->hDst + ov, dC, wc, hc);
+                const RowCopy out[3] = {{dstY, dstStY, st->hDst, dY, w, hh}, {dstU, dstStUV, st->hDst + ou, dC, wc, hc},
+                                        {dstV, dstStUV, st->hDst + ov, dC, wc, hc}};
+                copy_planes_par(out, 3);
             } else {
                 (void)hipStreamSynchronize(st->sK);
             }
@@ -1842,11 +1925,43 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
             return rc;
         }
     }
-    int rc = iqo_hip_resize(yp->y, srcStY, srcY, dstStY, dstY);
-    if (!rc)
-        rc = iqo_hip_resize(yp->c, srcStUV, srcU, dstStUV, dstU);
-    if (!rc)
-        rc = iqo_hip_resize(yp->c, srcStUV, srcV, dstStUV, dstV);
+    // large frames: the three planes through ONE host pipeline (their uploads, kernels and
+    // downloads overlap each other; one synchronisation per output chunk at the end)
+    const Plan &py = yp->y->p, &pc = yp->c->p;
+    const size_t sY = (static_cast<size_t>(py.srcW) + 15) & ~size_t(15), sC = (static_cast<size_t>(pc.srcW) + 15) & ~size_t(15);
+    const size_t dY = (static_cast<size_t>(py.dstW) + 15) & ~size_t(15), dC = (static_cast<size_t>(pc.dstW) + 15) & ~size_t(15);
+    const size_t oU = sY * static_cast<size_t>(py.srcH), oV = oU + sC * static_cast<size_t>(pc.srcH);
+    const size_t sBytes = oV + sC * static_cast<size_t>(pc.srcH);
+    const size_t ou = dY * static_cast<size_t>(py.dstH), ov = ou + dC * static_cast<size_t>(pc.dstH);
+    const size_t dBytes = ov + dC * static_cast<size_t>(pc.dstH);
+    DeviceGuard guard(yp->y->device);
+    if (!guard.ok())
+        return IQO_HIP_ENODEV;
+    HostStage *st = acquire_stage(yp->y->device);
+    if (!st)
+        return IQO_HIP_EHIP;
+    int rc = IQO_HIP_OK;
+    if (grow_device(&st->dSrc, &st->dSrcCap, sBytes) || grow_device(&st->dDst, &st->dDstCap, dBytes))
+        rc = IQO_HIP_ENOMEM;
+    const bool pinY = is_pinned_host(srcY), pinU = is_pinned_host(srcU), pinV = is_pinned_host(srcV);
+    const bool pinYd = is_pinned_host(dstY), pinUd = is_pinned_host(dstU), pinVd = is_pinned_host(dstV);
+    if (!rc && !(pinY && pinU && pinV) && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
+        rc = IQO_HIP_ENOMEM;
+    if (!rc && !(pinYd && pinUd && pinVd) && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
+        rc = IQO_HIP_ENOMEM;
+    if (!rc) {
+        HostPlane pl[3] = {{yp->y, srcStY, srcY, dstStY, dstY, 0, 0, sY, dY, pinY, pinYd},
+                           {yp->c, srcStUV, srcU, dstStUV, dstU, oU, ou, sC, dC, pinU, pinUd},
+                           {yp->c, srcStUV, srcV, dstStUV, dstV, oV, ov, sC, dC, pinV, pinVd}};
+        rc = host_pipeline(st, pl, 3);
+    }
+    if (rc) {
+        (void)hipStreamSynchronize(st->sIn);
+        (void)hipStreamSynchronize(st->sIn2);
+        (void)hipStreamSynchronize(st->sK);
+        (void)hipStreamSynchronize(st->sOut);
+    }
+    release_stage(st);
     return rc;
 }
 

@@ -3381,8 +3381,11 @@ struct RyxArgs {
 #ifndef IQO_RYX_WPE
 #define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
 #endif
+#ifndef IQO_RYX_WPE_WIDE
+#define IQO_RYX_WPE_WIDE 4  // ... for windows of more than 20 rows (Lanczos-8 / -9 2:1; variant builds: 2)
+#endif
 template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ, int CPT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQO_RYX_WPE_WIDE : IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
 {
     static_assert(CPT % 2 == 0 && (!ADJ || CPT == 2), "output columns per thread: pairs");
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
@@ -3554,21 +3557,37 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // (the splats arrive in cy, loaded before the barrier that precedes the pass: scalar loads
     // share the lgkm counter with the LDS reads, and waiting for them after the barrier would
     // also wait for the row's LDS reads)
-    auto coefs = [&](auto jc, uint32_t (&cy)[T]) {
+    // Lanczos 2:1 (one phase, symmetric window: plan.cpp build_ryx checks it): mirrored rows are
+    // summed first (widened bytes: <= 510 per half, one v_add_u32 for both halves), then one packed
+    // MAC per pair -- T / 2 MACs and T / 2 adds instead of T MACs; the low 16 bits of
+    // c (a + b) are those of c a + c b, the reference's int16 wrap
+    constexpr bool SYMV = LZ && P == 2 && Q == 1;
+    constexpr int TC = SYMV ? T / 2 : T;  // row coefficients the pass reads
+    static_assert(!SYMV || T % 2 == 0, "symmetric 2:1 windows have an even tap count");
+    auto coefs = [&](auto jc, uint32_t (&cy)[TC]) {
         constexpr int j = decltype(jc)::value;
 #pragma unroll
-        for (int k = 0; k < T; ++k)
+        for (int k = 0; k < TC; ++k)
             cy[k] = static_cast<uint32_t>(sld(d.rowCoef, j * T + k));
     };
-    auto vertical = [&](auto vc, auto jc, auto bc, int g, const uint32_t (&cy)[T]) {
+    auto vertical = [&](auto vc, auto jc, auto bc, int g, const uint32_t (&cy)[TC]) {
         constexpr int v = decltype(vc)::value, j = decltype(jc)::value, B = decltype(bc)::value;
         constexpr int S0 = (P * j) / Q;
         const int y = Q * (mLo + g) + j;
         uint32_t W[2] = {0u, 0u};
+        if constexpr (SYMV) {
 #pragma unroll
-        for (int k = 0; k < T; ++k) {
-            W[0] = pk_mad(R[(P * v + S0 + k) % NW][0], cy[k], W[0]);
-            W[1] = pk_mad(R[(P * v + S0 + k) % NW][1], cy[k], W[1]);
+            for (int k = 0; k < TC; ++k) {
+                const int ra = (P * v + S0 + k) % NW, rb = (P * v + S0 + T - 1 - k) % NW;
+                W[0] = pk_mad(R[ra][0] + R[rb][0], cy[k], W[0]);
+                W[1] = pk_mad(R[ra][1] + R[rb][1], cy[k], W[1]);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < T; ++k) {
+                W[0] = pk_mad(R[(P * v + S0 + k) % NW][0], cy[k], W[0]);
+                W[1] = pk_mad(R[(P * v + S0 + k) % NW][1], cy[k], W[1]);
+            }
         }
         if (LZ && (y < d.m0 || y >= d.m1)) {
             // masked border row (uniform, rare): rows outside the image read as zero
@@ -3583,7 +3602,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
     // prologue: group 0's rows, output row 0 into buffer 0
     enter_group(std::integral_constant<int, 0>{}, 0);
     {
-        uint32_t cy0[T];
+        uint32_t cy0[TC];
         coefs(std::integral_constant<int, 0>{}, cy0);
         vertical(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, 0,
                  cy0);
@@ -3602,7 +3621,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(IQO_RYX_WPE
             if (g >= nG)
                 return;  // whole workgroup
             constexpr int rn = (r + 1) % UQ, vn = rn / Q, jn = rn % Q;
-            uint32_t cyn[T];  // the next row's splats, complete at the barrier
+            uint32_t cyn[TC];  // the next row's splats, complete at the barrier
             coefs(std::integral_constant<int, jn>{}, cyn);
             if (IQO_RYX_EXP != 3)  // experiment 3: no barrier (timing only)
                 __syncthreads();
@@ -4954,11 +4973,21 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
             // (C2 x256: 24 bands 0.525 ms, 48 0.510, 96 0.515, 135 0.530; C1 x4096 (320 columns):
             // 2 bands 0.385, 5 0.366, 10 0.378).  Shorter bands keep the concurrently read source
             // window compact; longer ones pay less per-band prologue, which weighs more on narrow rows.
+            // Round 5, at a steady GPU clock (after the power-management transient a streaming
+            // launch starts with, profiles/r05/clock_transient.txt): the Lanczos-2/3 windows (NY <= 10)
+            // want bands of ~12 rows on rows of >= 640 outputs -- C2 x1024 1.936 ms at 50 bands of 22
+            // rows, 1.879 at 90 of 12 (frac 0.686 -> 0.706), x256 0.495 -> 0.480; 1080p -> 540p
+            // Lanczos-2 -2.6 % -- and ~24 on narrower rows (C1 x4096: 5 bands 0.331 ms, 10 bands
+            // 0.318, 20 bands 0.324); the 12- and 16-row windows keep ~22-row bands (Lanczos-4 4K:
+            // 50 bands 0.267 ms, 90 bands 0.270), their per-band halo being larger
+            // (profiles/r05/steady_streamer_bands.txt)
             const int64_t want = static_cast<int64_t>(l.rounds > 0 ? l.rounds : 6) * (resident / wpr);
             const int64_t byRounds = (want + io.frames - 1) / io.frames;
-            const int rowsMax = std::min(48, std::max(22, 22 * 1920 / std::max(1, l.dstW)));
+            const int rowsMax = l.NY <= 10 ? (l.dstW >= 640 ? 12 : 24)
+                                           : std::min(48, std::max(22, 22 * 1920 / std::max(1, l.dstW)));
+            const int rowsMin = l.NY <= 10 ? 12 : 16;
             bands = static_cast<int>(std::min<int64_t>(std::max<int64_t>(byRounds, (rows + rowsMax - 1) / rowsMax),
-                                                       std::max(1, rows / 16)));
+                                                       std::max(1, rows / rowsMin)));
         } else {
             bands = choose_bands(rows, io.frames, wpr, resident, l.NY - 2);
         }

@@ -1480,6 +1480,13 @@ void build_ryx(const Plan &p, RyxTables *t)
             }
             t->rowCoef[static_cast<size_t>(j * TK + w)] = (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u;
         }
+    // Lanczos 2:1 (one phase): the kernel pair-sums mirrored window rows before the packed MAC
+    // (kernels.hip ryx_kernel SYMV), so its window must be symmetric -- the reference's 2:1 tables
+    // are, and the zero-tap trim is symmetric too; anything else takes the other kernels
+    if (p.method == kLanczos && P == 2 && Q == 1)
+        for (int w = 0; w < TK; ++w)
+            if (t->rowCoef[static_cast<size_t>(w)] != t->rowCoef[static_cast<size_t>(TK - 1 - w)])
+                return;
     int m0 = 0, m1 = p.dstH;
     if (p.method == kLanczos) {
         m0 = -1;

@@ -21,10 +21,10 @@ KERNELS = {"lanczos_stream": "lanczos_s", "area_int": "area_int_kernel",  # lanc
            "linear_up2": "linear_up2_kernel", "general": "general_kernel", "tile": "tile_kernel",
            "walk": "walk_kernel", "lanczos_up2": "lanczos_up2_kernel", "lanczos_d32": "lanczos_d32_kernel",
            "area_d32": "area_d32_kernel", "lanczos_d31": "lanczos_d31_kernel", "ryx": "ryx_kernel"}
-BENCH = {"c2": ("lanczos_stream", 256), "c3": ("area_int", 64), "c4": ("linear_up2", 256), "c1": ("lanczos_stream", 4096),
+BENCH = {"c2": ("lanczos_stream", 1024), "c3": ("area_int", 64), "c4": ("linear_up2", 256), "c1": ("lanczos_stream", 4096),
          "g1": ("lanczos_d32", 128), "g2": ("lanczos_up2", 32), "g3": ("area_d32", 128),
          "g4": ("lanczos_d31", 128), "g5": ("ryx", 256), "g6": ("area_int", 128),
-         "h1": ("area_int", 128, "linear_d2_kernel"), "h2": ("ryx", 128), "h3": ("ryx", 128), "h4": ("lanczos_up2", 64),
+         "h1": ("area_int", 128, "linear_d2_kernel"), "h2": ("ryx", 128), "h3": ("lanczos_stream", 128), "h4": ("lanczos_up2", 64),
          "h5": ("linear_up2", 64), "h6": ("ryx", 128)}
 
 

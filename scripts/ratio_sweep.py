@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Kernel time and HBM roofline fraction over common video scaling ratios, on fresh device batches
-(distinct batches cycled, >= 2.5 GB per cycle, as bench.py), each output checked against the oracle
-on one frame.  Output: one line per shape (profiles/r02/ratio_sweep.txt).
+(distinct batches cycled, >= 2.5 GB per cycle, as bench.py) after an ~80 ms settle of back-to-back
+launches per shape (steady GPU clock, round 5), each output checked against the oracle on one frame.
+Output: one line per shape (profiles/r05/ratio_sweep.txt).
 
   python scripts/ratio_sweep.py [--steps 20] [--match linear:1280x720] [--opt ratio_prefetch=1 ...]
 """
@@ -64,6 +65,7 @@ SHAPES = [
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=80.0, help="untimed back-to-back launches before the timing")
     ap.add_argument("--match", default="", help="only shapes whose 'method:srcWxsrcH->dstWxdstH' contains this")
     ap.add_argument("--opt", action="append", default=[], help="plan option key=value (tuning runs)")
     args = ap.parse_args()
@@ -93,6 +95,15 @@ def main():
         for i in range(2 * rot):
             launch(i % rot)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if args.settle_ms > 0:
+            # the GPU lowers its clock for ~10-20 ms after a streaming kernel starts (round 5,
+            # profiles/r05/clock_transient.txt): time the steady state after a continuous settle
+            e0.record(s)
+            launch(0)
+            e1.record(s)
+            torch.cuda.synchronize(dev)
+            for i in range(int(args.settle_ms / max(e0.elapsed_time(e1), 0.005))):
+                launch(i % rot)
         e0.record(s)
         for i in range(args.steps):
             launch(i % rot)
