@@ -3382,7 +3382,8 @@ struct RyxArgs {
 #define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
 #endif
 #ifndef IQO_RYX_WPE_WIDE
-#define IQO_RYX_WPE_WIDE 4  // ... for windows of more than 20 rows (Lanczos-8 / -9 2:1; variant builds: 2)
+#define IQO_RYX_WPE_WIDE 2  // ... for windows of more than 20 rows: Lanczos-8 / -9 2:1 spill at 4 (steady clock, 4K 2:1
+                            // x128: Lanczos-8 1.154 -> 0.533 ms, Lanczos-9 1.822 -> 0.567, profiles/r05/steady_check2.txt)
 #endif
 template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ, int CPT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQO_RYX_WPE_WIDE : IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)

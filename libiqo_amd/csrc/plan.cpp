@@ -1467,7 +1467,12 @@ void build_ryx(const Plan &p, RyxTables *t)
     // the kernel window of output (m, j): TK rows from P m + floor(P j / Q) + off, ending no later
     // than the reference's windows (a downscale: taps [lo, lo + TK) of every phase, lo = the
     // leading zero taps or fewer)
-    const int off = std::min(lowest, maxEnd - TK);
+    int off = std::min(lowest, maxEnd - TK);
+    // Lanczos 2:1 (symmetric window, below): a window wider than the nonzero taps is padded evenly
+    // on both sides (an instantiation with more taps, picked for its column pairs)
+    if (p.method == kLanczos && P == 2 && Q == 1 && (TK - TE) % 2 == 0 && lowest - (TK - TE) / 2 >= minOff &&
+        lowest - (TK - TE) / 2 + TK <= maxEnd)
+        off = lowest - (TK - TE) / 2;
     t->rowCoef.assign(static_cast<size_t>(Q * TK), 0u);
     for (int j = 0; j < Q; ++j)
         for (int k = 0; k < T; ++k) {

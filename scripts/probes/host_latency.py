@@ -45,3 +45,27 @@ def cycle():
 
 
 print("I420 cycle, ctor in loop    ", timed(cycle))
+
+# Large I420 frames (C2: Y 3840x2160 -> 1920x1080, U/V 1920x1080 -> 960x540, Lanczos-3): the
+# three-plane host pipeline from pageable and from pinned user buffers (pinned: no staging copy),
+# and the Y plane alone, to separate staging, PCIe and the pipeline's own overhead.
+import torch  # noqa: E402
+
+W, H, w, h = 3840, 2160, 1920, 1080
+for kind in ("pageable", "pinned"):
+    def mk(shape, fill=None):
+        t = torch.zeros(shape, dtype=torch.uint8)
+        if kind == "pinned":
+            t = t.pin_memory()
+        a = t.numpy()
+        if fill is not None:
+            a[...] = fill
+        return t, a
+    (_, Yb), (_, Ub), (_, Vb) = mk((H, W), rng.integers(0, 256, (H, W), dtype=np.uint8)), \
+        mk((H // 2, W // 2), 7), mk((H // 2, W // 2), 9)
+    (_, yb), (_, ub), (_, vb) = mk((h, w)), mk((h // 2, w // 2)), mk((h // 2, w // 2))
+    yr = libiqo_amd.Yuv420Resizer("lanczos", 3, W, H, w, h)
+    print("C2 I420 %-8s (plan reused) " % kind,
+          timed(lambda: yr.resize(W, Yb, W // 2, Ub, Vb, w, yb, w // 2, ub, vb), n=40))
+    rY = libiqo_amd.LanczosResizer(3, W, H, w, h)
+    print("C2 Y     %-8s              " % kind, timed(lambda: rY.resize(W, Yb, w, yb), n=40))
