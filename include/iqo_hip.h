@@ -62,7 +62,9 @@ enum {
     IQO_KERNEL_LANCZOS_U23 = 9, /* exact 2:3 Lanczos-3 upscale: register-window streamer, borders in-kernel */
     IQO_KERNEL_LINEAR_U23 = 10, /* exact 2:3 Linear upscale: clamped halo, no border code */
     IQO_KERNEL_LANCZOS_D31 = 11, /* exact 3:1 Lanczos-2/3 downscale: register window, symmetric taps, borders in-kernel */
-    IQO_KERNEL_RYX = 12          /* exact vertical ratio (9:4), tabled columns: register window + LDS work row */
+    IQO_KERNEL_RYX = 12,         /* exact vertical ratio (9:4), tabled columns: register window + LDS work row */
+    IQO_KERNEL_RYG = 13          /* downscales by 1..2 (e.g. 1080 -> 768 rows), tabled rows and columns: shifting
+                                    register window + LDS work row */
 };
 
 typedef struct iqo_hip_plan iqo_hip_plan;
@@ -106,9 +108,9 @@ int iqo_hip_plan_prepare(iqo_hip_plan *plan);
  * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
  * IQO_KERNEL_GENERAL instead of IQO_KERNEL_TILE / _WALK), "walk" (0: IQO_KERNEL_TILE instead of
  * IQO_KERNEL_WALK / _LANCZOS_UP2; default 1), "up2" (0: IQO_KERNEL_WALK instead of
- * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" / "l23" / "d31" / "ryx" (0: the
+ * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" / "l23" / "d31" / "ryx" / "ryg" (0: the
  * walker or tile kernel instead of IQO_KERNEL_LANCZOS_D32 / _AREA_D32 / _LANCZOS_U23 /
- * _LINEAR_U23 / _LANCZOS_D31 / _RYX; default 1), "tile_rows" (output rows per tile, 0 = auto),
+ * _LINEAR_U23 / _LANCZOS_D31 / _RYX / _RYG; default 1), "tile_rows" (output rows per tile, 0 = auto),
  * "stack" (0 / 1 / 2: narrow frames side by side in one workgroup off / where a frame fills at
  * most half a wave (default) / from two frames per workgroup), "rounds" (block-shared streamer
  * band count in rounds of resident workgroups, 0 = 6), "prefetch", "lin_prefetch",

@@ -20,7 +20,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # LIBIQO_AMD_LIB selects an alternative build of the same library (A/B experiments only)
 LIB_PATH = os.environ.get("LIBIQO_AMD_LIB") or os.path.join(PKG_DIR, "libiqo_hip.so")
 
-KERNELS = {0: "general", 1: "lanczos_stream", 2: "area_int", 3: "linear_up2", 4: "tile", 5: "walk", 6: "lanczos_up2", 7: "lanczos_d32", 8: "area_d32", 9: "lanczos_u23", 10: "linear_u23", 11: "lanczos_d31", 12: "ryx"}
+KERNELS = {0: "general", 1: "lanczos_stream", 2: "area_int", 3: "linear_up2", 4: "tile", 5: "walk", 6: "lanczos_up2", 7: "lanczos_d32", 8: "area_d32", 9: "lanczos_u23", 10: "linear_u23", 11: "lanczos_d31", 12: "ryx", 13: "ryg"}
 _METHODS = {"lanczos": 0, "area": 1, "linear": 2}
 
 _c_sz = ctypes.c_size_t

@@ -88,6 +88,10 @@ struct iqo_hip_plan {
     iqo_amd::RyxTables ryx;
     uint32_t *dRyxRowCoef = nullptr, *dRyxColCoef = nullptr;
     int4 *dRyxCols = nullptr;
+    int2 *dRyxRowRec = nullptr;  // general-row tables (ryx.general: the ryg kernel)
+    bool useRyg = true;
+    int hostStage = 0;  // host-pointer path, frames >= 4 MiB: 0 the runtime's own pageable copies, 1 our pinned
+                        // staging pipeline (host_pipeline), for A/B
     bool useD32 = true;
     bool useD31 = true;
     bool useRyx = true;
@@ -504,8 +508,18 @@ int upload_exact(iqo_hip_plan *h)
     iqo_amd::build_d32(h->p, h->wt, &h->dt);
     iqo_amd::build_d31(h->p, &h->t31);
     iqo_amd::build_ryx(h->p, &h->ryx);
+    if (!h->ryx.ok)
+        iqo_amd::build_ryg(h->p, &h->ryx);  // general rows (no exact P:Q)
     if (h->ryx.ok && ryx_dev(h).parts == 0)
         h->ryx = iqo_amd::RyxTables();  // no column split fits the workgroup limits
+    if (h->ryx.ok && h->ryx.general) {
+        std::vector<int2> rr(h->ryx.rowRec.size() / 2);
+        for (size_t i = 0; i < rr.size(); ++i)
+            rr[i] = make_int2(h->ryx.rowRec[2 * i], h->ryx.rowRec[2 * i + 1]);
+        const int rc2 = upload(h, &h->dRyxRowRec, rr.data(), rr.size());
+        if (rc2)
+            return rc2;
+    }
     if (h->ryx.ok) {
         std::vector<int4> rc(h->ryx.cols.size() / 4);
         for (size_t i = 0; i < rc.size(); ++i)
@@ -622,6 +636,8 @@ void reset_options(iqo_hip_plan *h)
     h->ratioAlt = 1;
     h->chunkFrames = 0;
     h->useTile = h->useWalk = h->useUp2 = h->useD32 = h->useD31 = h->useRyx = h->useL23 = h->useU23 = h->useA32 = true;
+    h->useRyg = true;
+    h->hostStage = 0;
     if (h->tt.ok) {  // option "tile_rows"
         h->tt.TH = h->tileTH0;
         h->tt.srcRows = h->tileSrcRows0;
@@ -1044,6 +1060,34 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     return d;
 }
 
+// The general-row kernel's view: ryx_dev's column split and tables plus the row records.
+iqo_amd::RygDev ryg_dev(const iqo_hip_plan *h)
+{
+    const iqo_amd::RyxDev x = ryx_dev(h);
+    iqo_amd::RygDev d;
+    d.lanczos = x.lanczos;
+    d.srcW = x.srcW;
+    d.srcH = x.srcH;
+    d.dstW = x.dstW;
+    d.dstH = x.dstH;
+    d.taps = x.taps;
+    d.NP = x.NP;
+    d.m0 = x.m0;
+    d.m1 = x.m1;
+    std::memcpy(d.yM, x.yM, sizeof d.yM);
+    std::memcpy(d.yS, x.yS, sizeof d.yS);
+    d.rowRec = h->dRyxRowRec;
+    d.rowCoef = x.rowCoef;
+    d.cols = x.cols;
+    d.colCoef = x.colCoef;
+    d.parts = x.parts;
+    d.threads = x.threads;
+    std::memcpy(d.xs, x.xs, sizeof d.xs);
+    std::memcpy(d.cs, x.cs, sizeof d.cs);
+    std::memcpy(d.ce, x.ce, sizeof d.ce);
+    return d;
+}
+
 iqo_amd::L23Dev l23_dev(const iqo_hip_plan *h)
 {
     iqo_amd::L23Dev d;
@@ -1120,7 +1164,13 @@ iqo_amd::GeneralDev general_dev(const iqo_hip_plan *h)
 // The defaults end in split_min(512), the widest split, so when they fit every option does.
 bool ryx_usable(const iqo_hip_plan *h)
 {
-    return h->ryx.ok && h->useRyx && ryx_dev(h).parts > 0;
+    return h->ryx.ok && !h->ryx.general && h->useRyx && ryx_dev(h).parts > 0;
+}
+
+// ... and its general-row variant (build_ryg)
+bool ryg_usable(const iqo_hip_plan *h)
+{
+    return h->ryx.ok && h->ryx.general && h->useRyg && ryx_dev(h).parts > 0;
 }
 
 // The kernel family a full-frame call with aligned pointers and strides runs.
@@ -1147,6 +1197,10 @@ int plan_kernel(const iqo_hip_plan *h)
         k = IQO_KERNEL_LANCZOS_U23;
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->lt.ok && h->useL23)
         k = IQO_KERNEL_LINEAR_U23;
+    // general rows last: only what no exact-ratio kernel takes
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE || (k == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
+        ryg_usable(h))
+        k = IQO_KERNEL_RYG;
     return k;
 }
 
@@ -1200,6 +1254,10 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->lt.ok && h->useL23 &&
         aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LINEAR_U23;
+    // general rows last (dword loads, byte stores)
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE || (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
+        aligned(src, 4, srcSt, srcFrameSt) && ryg_usable(h))
+        kernel = IQO_KERNEL_RYG;
     return kernel;
 }
 
@@ -1243,7 +1301,7 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
 
     const int kernel = kernel_for_layout(h, src, srcSt, srcFrameSt, dst, dstSt, dstFrameSt);
     if (kernel == IQO_KERNEL_TILE || kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_RYX ||
-        kernel == IQO_KERNEL_GENERAL) {
+        kernel == IQO_KERNEL_RYG || kernel == IQO_KERNEL_GENERAL) {
         const int rc = ensure_tables(h);
         if (rc)
             return rc;
@@ -1297,6 +1355,8 @@ int run_band(iqo_hip_plan *h, size_t nFrames, size_t r0, size_t rows, size_t src
             e = iqo_amd::launch_d31(d31_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_RYX)
             e = iqo_amd::launch_ryx(ryx_dev(h), io, rb, re, h->bands, s);
+        else if (kernel == IQO_KERNEL_RYG)
+            e = iqo_amd::launch_ryg(ryg_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_AREA_D32)
             e = iqo_amd::launch_a32(a32_dev(h), io, rb, re, h->bands, s);
         else if (kernel == IQO_KERNEL_LANCZOS_U23)
@@ -1514,6 +1574,16 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->ratioPrefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
+    if (!std::strcmp(key, "host_stage")) {  // host-pointer path of large frames (speed only): 0 the runtime's
+        if (value < 0 || value > 1)              // pageable copies, 1 the pinned staging pipeline
+            return IQO_HIP_EINVAL;
+        h->hostStage = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryg")) {  // 0: general-row downscales (1 .. 2 : 1) use the wave walker / tile kernel
+        h->useRyg = value != 0;
+        return IQO_HIP_OK;
+    }
     if (!std::strcmp(key, "ryx")) {  // 0: exact-vertical-ratio downscales use the general kernels
         h->useRyx = value != 0;
         return IQO_HIP_OK;
@@ -1678,6 +1748,48 @@ int host_pipeline(HostStage *st, HostPlane *planes, int nPlanes)
     return IQO_HIP_OK;
 }
 
+// Large frames from pageable memory, the default: the HIP runtime's own pageable copies (it stages
+// through its pinned buffers at close to the PCIe rate: 44 GB/s H2D for a 12 MB plane set against
+// 53 GB/s from pinned memory, profiles/r05/pcie_probe.json), every plane's upload first, then the
+// kernels, then the downloads, one stream, one synchronisation.  Our own staging pipeline
+// (host_pipeline: pool memcpy into pinned memory + DMA per band) spent more host time on its per-band
+// copies, events and launches than the transfers take (C2 Y 0.43 ms, I420 0.58 ms).
+int host_direct(HostStage *st, HostPlane *planes, int nPlanes)
+{
+    for (int q = 0; q < nPlanes; ++q) {
+        const HostPlane &P = planes[q];
+        const Plan &p = P.h->p;
+        const size_t W = static_cast<size_t>(p.srcW), H = static_cast<size_t>(p.srcH);
+        const hipError_t e = (P.srcSt == W && P.sPitch == W)
+                                 ? hipMemcpyAsync(st->dSrc + P.sOff, P.src, W * H, hipMemcpyHostToDevice, st->sK)
+                                 : hipMemcpy2DAsync(st->dSrc + P.sOff, P.sPitch, P.src, P.srcSt, W, H,
+                                                    hipMemcpyHostToDevice, st->sK);
+        if (e != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
+    for (int q = 0; q < nPlanes; ++q) {
+        const HostPlane &P = planes[q];
+        const Plan &p = P.h->p;
+        const size_t sBytes = P.sPitch * static_cast<size_t>(p.srcH), dBytes = P.dPitch * static_cast<size_t>(p.dstH);
+        const int rc = run_band(P.h, 1, 0, static_cast<size_t>(p.dstH), 0, P.sPitch, sBytes, st->dSrc + P.sOff, P.dPitch,
+                                dBytes, st->dDst + P.dOff, st->sK);
+        if (rc)
+            return rc;
+    }
+    for (int q = 0; q < nPlanes; ++q) {
+        const HostPlane &P = planes[q];
+        const Plan &p = P.h->p;
+        const size_t w = static_cast<size_t>(p.dstW), hh = static_cast<size_t>(p.dstH);
+        const hipError_t e = (P.dstSt == w && P.dPitch == w)
+                                 ? hipMemcpyAsync(P.dst, st->dDst + P.dOff, w * hh, hipMemcpyDeviceToHost, st->sK)
+                                 : hipMemcpy2DAsync(P.dst, P.dstSt, st->dDst + P.dOff, P.dPitch, w, hh,
+                                                    hipMemcpyDeviceToHost, st->sK);
+        if (e != hipSuccess)
+            return IQO_HIP_EHIP;
+    }
+    return hipStreamSynchronize(st->sK) == hipSuccess ? IQO_HIP_OK : IQO_HIP_EHIP;
+}
+
 static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
 {
     const Plan &p = h->p;
@@ -1723,7 +1835,7 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
         return IQO_HIP_OK;
     }
     HostPlane pl{h, srcSt, src, dstSt, dst, 0, 0, sPitch, dPitch, pinSrc, pinDst};
-    return host_pipeline(st, &pl, 1);
+    return h->hostStage || (pinSrc && pinDst) ? host_pipeline(st, &pl, 1) : host_direct(st, &pl, 1);
 }
 
 int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
@@ -1953,7 +2065,8 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
         HostPlane pl[3] = {{yp->y, srcStY, srcY, dstStY, dstY, 0, 0, sY, dY, pinY, pinYd},
                            {yp->c, srcStUV, srcU, dstStUV, dstU, oU, ou, sC, dC, pinU, pinUd},
                            {yp->c, srcStUV, srcV, dstStUV, dstV, oV, ov, sC, dC, pinV, pinVd}};
-        rc = host_pipeline(st, pl, 3);
+        rc = yp->y->hostStage || (pinY && pinU && pinV && pinYd && pinUd && pinVd) ? host_pipeline(st, pl, 3)
+                                                                                    : host_direct(st, pl, 3);
     }
     if (rc) {
         (void)hipStreamSynchronize(st->sIn);
@@ -2204,6 +2317,8 @@ int iqo_host_kernel_for(int method, unsigned degree, size_t srcW, size_t srcH, s
     iqo_amd::build_d32(h.p, h.wt, &h.dt);
     iqo_amd::build_d31(h.p, &h.t31);
     iqo_amd::build_ryx(h.p, &h.ryx);
+    if (!h.ryx.ok)
+        iqo_amd::build_ryg(h.p, &h.ryx);
     if (h.ryx.ok && ryx_dev(&h).parts == 0)
         h.ryx = iqo_amd::RyxTables();
     iqo_amd::build_a32(h.p, &h.at);

@@ -3706,6 +3706,230 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
     }
 }
 
+// ================================================================ general-row ratio kernel
+//
+// ryx_kernel's layout for downscales whose rows shrink by more than 1 and at most 2 with no small
+// exact ratio (plan.cpp build_ryg), e.g. 1080 -> 768 rows (45:32) or 1080 -> 576 (15:8), which
+// otherwise run the wave walker.  One workgroup per (row band, frame, column part); thread = 4 source
+// columns.  Output row y has a record {first window row s(y), offset of its phase's taps}
+// (IQO*ResizerImpl_Generic.cpp's row driver: LinearIterator source row and y mod rDst phase,
+// Lanczos :369-454, Area :250-294; masked Lanczos border rows :464-490 divided in place as in
+// ryx_kernel).  The thread's register window R holds rows s(y) .. s(y) + T - 1 widened to u16
+// pairs at FIXED names: moving to row y + 1 shifts it by s(y+1) - s(y), 1 or 2 rows (a uniform
+// branch with register moves), and the incoming rows come from a FIFO of raw dwords loaded PD
+// output rows ahead -- always the last two rows of that row's window, so every output row issues
+// exactly two loads (branch-free memory stream, exact vmcnt waits; when the window moves by one row
+// the first of the two is the row the previous pair brought, an L2 hit).  Vertical: T packed MACs
+// per u16 pair; horizontal, LDS work rows, the next row's vertical pass under this row's LDS
+// reads, column tables and stores: as ryx_kernel with two output columns per thread.
+struct RygArgs {
+    RygDev d;
+    Io io;
+    int rowBegin, rowEnd, rowsPerBand, bands;
+    int srcBytes, dstBytes;
+    unsigned nBlocks;
+};
+
+template <bool LZ, int T, int NP, int PD>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryg_kernel(RygArgs a)
+{
+    constexpr int OOB = 0x7ff00000;
+    constexpr int PADB = 2 * kRyxPadK;  // work-row byte padding left of column 0
+    static_assert(PD % 2 == 0 && T >= 2, "the unrolled trip covers both work-row buffers");
+    const RygDev &d = a.d;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int t = static_cast<int>(threadIdx.x);
+    const unsigned blk0 = xcd_spread(blockIdx.x, gridDim.x);
+    if (blk0 >= a.nBlocks)
+        return;  // whole workgroup
+    const int part = static_cast<int>(blk0 % static_cast<unsigned>(d.parts));
+    const unsigned blk = blk0 / static_cast<unsigned>(d.parts);
+    const int cLo = d.parts > 1 ? d.cs[part] : 0, cHi = d.parts > 1 ? d.ce[part] : d.srcW;
+    const int xLo = d.parts > 1 ? d.xs[part] : 0, xHi = d.parts > 1 ? d.xs[part + 1] : d.dstW;
+    const int band = static_cast<int>(blk % static_cast<unsigned>(a.bands));
+    const int frame = static_cast<int>(blk / static_cast<unsigned>(a.bands));
+    const int y0 = a.rowBegin + band * a.rowsPerBand, y1 = min(y0 + a.rowsPerBand, a.rowEnd);
+    if (y0 >= y1)
+        return;  // whole workgroup
+    const int nRows = y1 - y0;
+
+    const uint8_t *srcFrame = a.io.src + static_cast<int64_t>(frame) * a.io.srcFrameSt;
+    uint8_t *dstFrame = a.io.dst + static_cast<int64_t>(frame) * a.io.dstFrameSt;
+    const __amdgpu_buffer_rsrc_t srcR =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(srcFrame), 0, a.srcBytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
+    const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
+    const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
+    const int rLo = max(0, srcRow0), rHi = min(d.srcH, a.io.srcRowEnd);  // loadable source rows
+    const int span = cHi - cLo;
+    const int voff = 4 * t < span ? cLo + 4 * t : OOB;
+
+    // work rows: two buffers of (pad + span + pad) u16, zero padding written once
+    const int pitch = PADB + 2 * span + PADB;
+    for (int i = t; i < 2 * (PADB / 4); i += static_cast<int>(blockDim.x)) {
+        const int buf = i / (PADB / 4), k = i % (PADB / 4);
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * span + 4 * k) = 0u;
+    }
+    // the thread's output columns xLo + t and xLo + half + t (neighbouring lanes one column apart)
+    const int half = (xHi - xLo + 1) / 2;
+    int xc[2], aoff[2], sh[2], stoff[2];
+    uint32_t cf[2][NP], mm[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        xc[k] = xLo + k * half + t;
+        const int x = min(xc[k], xHi - 1);
+        const int4 c = d.cols[x];
+        aoff[k] = c.x - 2 * cLo;
+        mm[k] = static_cast<uint32_t>(c.y);
+        sh[k] = c.z;
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+            cf[k][q] = d.colCoef[x * NP + q];
+        stoff[k] = t < half && xc[k] < xHi ? xc[k] : OOB;
+    }
+    const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
+
+    auto load_row = [&](int r) -> uint32_t {
+        const bool in = r >= rLo && r < rHi;
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? (r - srcRow0) * srcSt : OOB), 0, 0);
+    };
+    auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
+        W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
+        W[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
+    };
+    const int recLast = a.rowEnd - 1;
+    auto rec_s = [&](int y) { return sld(d.rowRec, 2 * min(y, recLast)); };
+    auto rec_c = [&](int y) { return sld(d.rowRec, 2 * min(y, recLast) + 1); };
+
+    // window of row y0, the FIFO (slot i: the last two window rows of row y0 + 1 + i)
+    int curS = rec_s(y0);
+    uint32_t R[T][2];
+#pragma unroll
+    for (int k = 0; k < T; ++k)
+        widen(load_row(curS + k), R[k]);
+    uint32_t F[PD][2];
+#pragma unroll
+    for (int i = 0; i < PD; ++i) {
+        const bool use = i + 1 < nRows;
+        const int sF = rec_s(y0 + 1 + i);
+        F[i][0] = load_row(use ? sF + T - 2 : -1);
+        F[i][1] = load_row(use ? sF + T - 1 : -1);
+    }
+    auto vertical = [&](auto bc, int y, const uint32_t (&cy)[T]) {
+        constexpr int B = decltype(bc)::value;
+        uint32_t W[2] = {0u, 0u};
+#pragma unroll
+        for (int k = 0; k < T; ++k) {
+            W[0] = pk_mad(R[k][0], cy[k], W[0]);
+            W[1] = pk_mad(R[k][1], cy[k], W[1]);
+        }
+        if (LZ && (y < d.m0 || y >= d.m1)) {
+            // masked border row (uniform, rare): rows outside the image read as zero
+            const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 15);
+            W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
+            W[1] = ydiv2(W[1], d.yM[side][i], d.yS[side][i]);
+        }
+        if (4 * t < span)
+            *reinterpret_cast<uint2 *>(lds + B * pitch + PADB + 8 * t) = make_uint2(W[0], W[1]);
+    };
+    {
+        uint32_t cy0[T];
+        const int co = rec_c(y0);
+#pragma unroll
+        for (int k = 0; k < T; ++k)
+            cy0[k] = static_cast<uint32_t>(sld(d.rowCoef, co + k));
+        vertical(std::integral_constant<int, 0>{}, y0, cy0);
+    }
+    int nextS = rec_s(y0 + 1), nextC = rec_c(y0 + 1);  // record of the next row, one row ahead
+
+    for (int base = 0; base < nRows; base += PD) {
+        static_for<PD>([&](auto rc) {
+            constexpr int r = decltype(rc)::value, B = r & 1;
+            const int i = base + r;
+            if (i >= nRows)
+                return;  // whole workgroup
+            const int y = y0 + i;
+            const bool more = i + 1 < nRows;
+            // scalar loads before the barrier (they share lgkmcnt with the LDS reads after it)
+            uint32_t cyn[T];
+#pragma unroll
+            for (int k = 0; k < T; ++k)
+                cyn[k] = static_cast<uint32_t>(sld(d.rowCoef, nextC + k));
+            const int s2 = rec_s(y + 2), c2 = rec_c(y + 2), sF = rec_s(y + 1 + PD);
+            __syncthreads();
+            const uint8_t *wr = lds + B * pitch;
+            uint32_t w[2][NP];
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+#pragma unroll
+                for (int q = 0; q < NP; ++q)
+                    w[k][q] = reinterpret_cast<const uint32_t *>(wr + aoff[k])[q];
+            if (more) {
+                // the next row's window (FIFO slot r), the slot's reload, its vertical pass
+                if (nextS - curS == 2) {
+#pragma unroll
+                    for (int k = 0; k < T - 2; ++k) {
+                        R[k][0] = R[k + 2][0];
+                        R[k][1] = R[k + 2][1];
+                    }
+                    widen(F[r][0], R[T - 2]);
+                    widen(F[r][1], R[T - 1]);
+                } else {
+#pragma unroll
+                    for (int k = 0; k < T - 1; ++k) {
+                        R[k][0] = R[k + 1][0];
+                        R[k][1] = R[k + 1][1];
+                    }
+                    widen(F[r][1], R[T - 1]);
+                }
+                curS = nextS;
+            }
+            const bool useF = i + 1 + PD < nRows;
+            F[r][0] = load_row(useF ? sF + T - 2 : -1);
+            F[r][1] = load_row(useF ? sF + T - 1 : -1);
+            if (more)
+                vertical(std::integral_constant<int, B ^ 1>{}, y + 1, cyn);
+            nextS = s2;
+            nextC = c2;
+            // horizontal: the thread's two columns of row y
+            uint32_t packed;
+            if constexpr (LZ) {
+                int acc[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    acc[k] = sdot2_vv(w[k][0], cf[k][0], 1 << 19);
+#pragma unroll
+                    for (int q = 1; q < NP; ++q)
+                        acc[k] = sdot2(w[k][q], cf[k][q], acc[k]);
+                }
+                if (edgeT) {
+                    const uint32_t o0 = min(__umulhi(static_cast<uint32_t>(max(acc[0], 0)), mm[0]) >> sh[0], 255u);
+                    const uint32_t o1 = min(__umulhi(static_cast<uint32_t>(max(acc[1], 0)), mm[1]) >> sh[1], 255u);
+                    packed = opaque(o0) | (opaque(o1) << 8);
+                } else {
+                    packed = pack_lo(acc[0], acc[1]);  // sat_u8(acc >> 20) of both columns
+                }
+            } else {
+                int o[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    uint32_t acc = 1u << 22;
+#pragma unroll
+                    for (int q = 0; q < NP; ++q)
+                        acc = udot2(w[k][q], cf[k][q], acc);
+                    const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
+                    o[k] = u > 255 ? 255 : u;
+                }
+                packed = opaque(static_cast<uint32_t>(o[0])) | (opaque(static_cast<uint32_t>(o[1])) << 8);
+            }
+            const int rowOff = (y - dstRow0) * dstSt;
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff[0] + rowOff, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed >> 8), dstR, stoff[1] + rowOff, 0, 0);
+        });
+    }
+}
+
 // ================================================================ exact 2:3 Lanczos-3 upscale
 //
 // Lanczos-3 at exactly 3/2 (e.g. 1280x720 -> 1920x1080; plan.cpp build_u23).  Output y = 3m + j
@@ -4690,6 +4914,71 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     if (nBlocks >= (uint64_t(1) << 31))
         return hipErrorInvalidValue;
     RyxArgs a{d, io, rowBegin, rowEnd, groupBegin, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
+              static_cast<unsigned>(nBlocks)};
+    void *args[] = {&a};
+    return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(static_cast<unsigned>(threads)), args,
+                           static_cast<size_t>(ldsBytes), s);
+}
+
+hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
+{
+    if (rowEnd <= rowBegin || io.frames <= 0)
+        return hipSuccess;
+    if (d.srcW % 4 || d.srcW > 8192 || d.dstW > 4096 || !d.rowRec)
+        return hipErrorInvalidValue;
+    const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
+    const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;
+    if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
+        return hipErrorInvalidValue;
+    // instantiations (plan.cpp build_ryg kShapes): taps, column pairs; PD = 4 output rows ahead
+    struct Inst {
+        bool lz;
+        int T, NP;
+        const void *kern;
+    };
+#define IQO_RYG(LZ_, T_, NP_) {LZ_, T_, NP_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4>)}
+    static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 6),
+                                 IQO_RYG(true, 12, 7),
+                                 IQO_RYG(false, 2, 2), IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3)};
+#undef IQO_RYG
+    const void *kern = nullptr;
+    for (const Inst &k : kInst)
+        if (k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP)
+            kern = k.kern;
+    if (!kern || d.parts < 1 || d.parts > 16)
+        return hipErrorInvalidValue;
+    const int threads = d.threads > 0 ? d.threads : 512;
+    if (threads % 64 || threads > 512)
+        return hipErrorInvalidValue;
+    int maxSpan = d.srcW;
+    if (d.parts > 1) {
+        if (d.xs[0] != 0 || d.xs[d.parts] != d.dstW)
+            return hipErrorInvalidValue;
+        maxSpan = 0;
+        for (int k = 0; k < d.parts; ++k) {
+            if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > 2 * threads || d.cs[k] % 4 ||
+                d.cs[k] < 0 || d.ce[k] > d.srcW || d.ce[k] - d.cs[k] > 4 * threads || d.ce[k] <= d.cs[k])
+                return hipErrorInvalidValue;
+            maxSpan = std::max(maxSpan, d.ce[k] - d.cs[k]);
+        }
+    } else if (d.srcW > 4 * threads || d.dstW > 2 * threads) {
+        return hipErrorInvalidValue;
+    }
+    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
+    const int rows = rowEnd - rowBegin;
+    // bands: ~2.5 rounds of resident workgroups, >= 16 rows each
+    if (bands <= 0) {
+        const int64_t resident = std::max(1, resident_waves(kern, threads, ldsBytes) / (threads / 64));
+        const int64_t perBand = static_cast<int64_t>(io.frames) * d.parts;
+        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
+    }
+    bands = std::max(1, std::min(bands, rows));
+    const int rpb = (rows + bands - 1) / bands;
+    bands = (rows + rpb - 1) / rpb;
+    const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames) * static_cast<uint64_t>(d.parts);
+    if (nBlocks >= (uint64_t(1) << 31))
+        return hipErrorInvalidValue;
+    RygArgs a{d, io, rowBegin, rowEnd, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nBlocks)};
     void *args[] = {&a};
     return hipLaunchKernel(kern, dim3(static_cast<unsigned>(nBlocks)), dim3(static_cast<unsigned>(threads)), args,

@@ -142,6 +142,24 @@ struct RyxDev {
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
+// General-row variant (plan.hpp build_ryg; kernels.hip ryg_kernel): ryx's tabled columns and column
+// parts, rows from a per-row record table instead of an exact P:Q.
+struct RygDev {
+    bool lanczos;
+    int srcW, srcH, dstW, dstH;
+    int taps, NP;
+    int m0, m1;                  // Lanczos main rows; the others are masked border rows (magic_y)
+    uint32_t yM[2][16];
+    int yS[2][16];
+    const int2 *rowRec;          // dstH x {first window row, offset of the row's taps in rowCoef}
+    const uint32_t *rowCoef;     // phases x taps (c, c) splats
+    const int4 *cols;            // as RyxDev
+    const uint32_t *colCoef;
+    int parts, threads;
+    int xs[17], cs[16], ce[16];
+};
+hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
+
 // Exact 2:3 Lanczos-3 upscale (plan.hpp U23Tables).
 struct U23Dev {
     int srcW, srcH, dstW, dstH;

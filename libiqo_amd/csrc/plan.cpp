@@ -1389,6 +1389,8 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
     d->ok = true;
 }
 
+bool ryx_columns(const Plan &p, int NP, RyxTables *t);
+
 void build_ryx(const Plan &p, RyxTables *t)
 {
     *t = RyxTables();
@@ -1524,18 +1526,155 @@ void build_ryx(const Plan &p, RyxTables *t)
                 return;
         }
     }
-    // columns: the reference's window, made to start on an even column (a leading zero coefficient),
-    // NP pairs; masked Lanczos border taps outside the image meet the zero padding of the work row
+    if (!ryx_columns(p, NP, t))
+        return;
+    t->P = P;
+    t->Q = Q;
+    t->taps = TK;
+    t->off = off;
+    t->NP = NP;
+    t->m0 = m0;
+    t->m1 = m1;
+    t->ok = true;
+}
+
+void build_ryg(const Plan &p, RyxTables *t)
+{
+    *t = RyxTables();
+    // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart); widths
+    // as ryx_kernel
+    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
+        p.srcW < 16 || p.dstH < 4 || p.srcH <= p.dstH || p.srcH > 2 * p.dstH)
+        return;
+    const int T = p.y.taps;
+    // Lanczos: outer taps that are zero in every phase are dropped (as build_ryx)
+    int lo = 0, hi = T - 1;
+    if (p.method == kLanczos) {
+        lo = T;
+        hi = -1;
+        for (int j = 0; j < p.y.phases; ++j) {
+            const int32_t *c = &p.y.table[static_cast<size_t>(j * T)];
+            int a = 0, b = T - 1;
+            while (a < T && c[a] == 0)
+                ++a;
+            while (b > a && c[b] == 0)
+                --b;
+            if (a == T)
+                continue;
+            lo = std::min(lo, a);
+            hi = std::max(hi, b);
+        }
+        if (hi < lo)
+            return;
+    }
+    const int TE = hi - lo + 1;
+    // instantiated (method, taps, column pairs): kernels.hip launch_ryg
+    struct Shape {
+        int method, T, NP;
+    };
+    static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5}, {kLanczos, 10, 6}, {kLanczos, 12, 7},
+                                    {kArea, 2, 2},    {kArea, 3, 2},    {kArea, 3, 3}};
+    const Shape *best = nullptr;
+    for (const Shape &S : kShapes)
+        if (S.method == p.method && S.T >= TE && S.T <= T && p.x.taps + 1 <= 2 * S.NP &&
+            (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))
+            best = &S;
+    if (!best)
+        return;
+    const int TK = best->T, NP = best->NP;
+    const int off = std::min(lo, T - TK);  // kernel window: taps [off, off + TK) of the reference's
+    // per-phase taps as (c, c) splats
+    t->rowCoef.assign(static_cast<size_t>(p.y.phases) * TK, 0u);
+    for (int j = 0; j < p.y.phases; ++j)
+        for (int k = 0; k < T; ++k) {
+            const int32_t c = p.y.table[static_cast<size_t>(j * T + k)];
+            if (k < off || k >= off + TK) {
+                if (c != 0)
+                    return;
+                continue;
+            }
+            t->rowCoef[static_cast<size_t>(j * TK + k - off)] = (static_cast<uint32_t>(c) & 0xffffu) * 0x10001u;
+        }
+    // rows: {first window row, tap offset}; windows 1 or 2 rows apart; Lanczos main rows in one
+    // range [m0, m1) with their whole window in the image, at most 16 masked border rows per side
+    t->rowRec.assign(static_cast<size_t>(p.dstH) * 2, 0);
+    int m0 = 0, m1 = p.dstH;
+    if (p.method == kLanczos) {
+        m0 = -1;
+        m1 = -1;
+    }
+    for (int y = 0; y < p.dstH; ++y) {
+        const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
+        if (ci.kind == kIdentity || ci.tabOff % T)
+            return;
+        const int s0 = ci.srcO + off;
+        if (y > 0) {
+            const int adv = s0 - t->rowRec[static_cast<size_t>(2 * y - 2)];
+            if (adv < 1 || adv > 2)
+                return;
+        }
+        t->rowRec[static_cast<size_t>(2 * y)] = s0;
+        t->rowRec[static_cast<size_t>(2 * y + 1)] = ci.tabOff / T * TK;
+        if (p.method == kLanczos) {
+            const Window win = axis_window(p, p.y, y, false);
+            if (!win.border) {
+                if (win.start < 0 || win.start + T > p.srcH)
+                    return;
+                if (m0 < 0)
+                    m0 = y;
+                else if (m1 >= 0)
+                    return;
+            } else if (m0 >= 0 && m1 < 0) {
+                m1 = y;
+            }
+        } else if (s0 + TK > p.srcH + 1) {
+            return;  // (Area reads at most one row past the end, with weight 0: it loads as zero)
+        }
+    }
+    if (p.method == kLanczos) {
+        if (m0 < 0)
+            return;
+        if (m1 < 0)
+            m1 = p.dstH;
+        if (m0 > 16 || p.dstH - m1 > 16)
+            return;
+        for (int y = 0; y < p.dstH; ++y) {
+            if (y >= m0 && y < m1)
+                continue;
+            const Window win = axis_window(p, p.y, y, false);
+            const int side = y < m0 ? 0 : 1, i = side ? y - m1 : y;
+            if (!win.border || !magic_y(win.div, &t->yM[side][i], &t->yS[side][i]))
+                return;
+        }
+    }
+    if (!ryx_columns(p, NP, t))
+        return;
+    t->general = true;
+    t->P = 0;
+    t->Q = 0;
+    t->taps = TK;
+    t->off = off;
+    t->NP = NP;
+    t->m0 = m0;
+    t->m1 = m1;
+    t->ok = true;
+}
+
+// The tabled columns of ryx_kernel / ryg_kernel: the reference's window, made to start on an even
+// column (a leading zero coefficient), NP pairs; masked Lanczos border taps outside the image meet
+// the zero padding of the work row
+bool ryx_columns(const Plan &p, int NP, RyxTables *t)
+{
     t->cols.assign(static_cast<size_t>(p.dstW) * 4, 0);
     t->colCoef.assign(static_cast<size_t>(p.dstW) * NP, 0u);
     for (int x = 0; x < p.dstW; ++x) {
         const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
         if (ci.kind == kIdentity)
-            return;
+            return false;
         const int start = ci.srcO;
         const int a = start & ~1;  // even start (floor)
         if (a < -kRyxPad || a + 2 * NP > p.srcW + kRyxPad)
-            return;
+            return false;
         std::vector<int32_t> c(static_cast<size_t>(2 * NP), 0);
         for (int k = 0; k < p.x.taps; ++k)
             c[static_cast<size_t>(start - a + k)] = p.x.table[static_cast<size_t>(ci.tabOff + k)];
@@ -1547,21 +1686,14 @@ void build_ryx(const Plan &p, RyxTables *t)
         if (p.method == kLanczos) {
             const Window win = axis_window(p, p.x, x, true);
             if (!magic_x(win.border ? win.div : (1 << 20), &m, &sh))
-                return;
+                return false;
         }
         int32_t *cx = &t->cols[static_cast<size_t>(x) * 4];
         cx[0] = 2 * (a + kRyxPad);  // byte offset in the work row
         cx[1] = static_cast<int32_t>(m);
         cx[2] = sh;
     }
-    t->P = P;
-    t->Q = Q;
-    t->taps = TK;
-    t->off = off;
-    t->NP = NP;
-    t->m0 = m0;
-    t->m1 = m1;
-    t->ok = true;
+    return true;
 }
 
 void build_d31(const Plan &p, D31Tables *d)

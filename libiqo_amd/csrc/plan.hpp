@@ -265,10 +265,19 @@ struct RyxTables {
     std::vector<uint32_t> rowCoef;         // Q x taps (c, c) u16 splats: phase j's taps
     std::vector<int32_t> cols;             // dstW x 4: {work byte offset of the even start, magic, shift, 0}
     std::vector<uint32_t> colCoef;         // dstW x NP coefficient pairs from the even start
+    // general rows (build_ryg, kernels.hip ryg_kernel): no exact P:Q; every output row y has its own
+    // record {first window row, offset of its phase's taps in rowCoef} and consecutive windows
+    // start 1 or 2 rows apart (downscales of 1 .. 2 : 1)
+    bool general = false;
+    std::vector<int32_t> rowRec;           // dstH x 2
 };
 // Work-row padding (u16 entries) left of source column 0 in the kernel's LDS work row.
 constexpr int kRyxPad = 24;
 void build_ryx(const Plan &p, RyxTables *t);
+// The general-row variant of build_ryx (IQO_KERNEL_RYG): Lanczos and Area downscales whose rows
+// shrink by more than 1 and at most 2 (e.g. 1080 -> 768, 1080 -> 576) and that no exact-ratio
+// kernel takes.  Tabled rows and columns; the kernel's register window advances 1 or 2 rows.
+void build_ryg(const Plan &p, RyxTables *t);
 
 // Exact 2:3 Lanczos-3 upscale (kernels.hip lanczos_u23_kernel), e.g. 1280x720 -> 1920x1080.  In the
 // reference's tables for this ratio output y (x) = 3m + j takes phase j: j = 0 a single tap on

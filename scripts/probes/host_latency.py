@@ -51,6 +51,7 @@ print("I420 cycle, ctor in loop    ", timed(cycle))
 # and the Y plane alone, to separate staging, PCIe and the pipeline's own overhead.
 import torch  # noqa: E402
 
+assert torch.cuda.is_available()  # initialises the HIP runtime in torch before pin_memory()
 W, H, w, h = 3840, 2160, 1920, 1080
 for kind in ("pageable", "pinned"):
     def mk(shape, fill=None):
