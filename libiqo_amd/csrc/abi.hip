@@ -1040,6 +1040,16 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
         d.cpt = 2;
         d.parts = 0;
     }
+    // general rows (ryg) on rows of more than 1024 outputs: 4 output columns per thread, so one
+    // workgroup per row (or per half row) does the row's vertical pass once and has 4 columns of
+    // work per barrier (1080p -> 1366x768: 2 columns per thread took 4 parts of 256 threads)
+    if (t.general && d.dstW > 1024) {
+        d.cpt = 4;
+        if (split(2, 256) || split(1, 512) || split_min(512))
+            return d;
+        d.cpt = 2;
+        d.parts = 0;
+    }
     const int tw = h->ryxSplit == 2 ? 128 : h->ryxSplit == 3 ? 64 : 256;
     if (!(h->ryxSplit >= 2 && split_min(tw)) &&
         !(h->ryxSplit == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
@@ -1085,6 +1095,7 @@ iqo_amd::RygDev ryg_dev(const iqo_hip_plan *h)
     std::memcpy(d.xs, x.xs, sizeof d.xs);
     std::memcpy(d.cs, x.cs, sizeof d.cs);
     std::memcpy(d.ce, x.ce, sizeof d.ce);
+    d.cpt = x.cpt;
     return d;
 }
 
@@ -1198,8 +1209,7 @@ int plan_kernel(const iqo_hip_plan *h)
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->lt.ok && h->useL23)
         k = IQO_KERNEL_LINEAR_U23;
     // general rows last: only what no exact-ratio kernel takes
-    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE || (k == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
-        ryg_usable(h))
+    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && ryg_usable(h))
         k = IQO_KERNEL_RYG;
     return k;
 }
@@ -1255,8 +1265,7 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LINEAR_U23;
     // general rows last (dword loads, byte stores)
-    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE || (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
-        aligned(src, 4, srcSt, srcFrameSt) && ryg_usable(h))
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && aligned(src, 4, srcSt, srcFrameSt) && ryg_usable(h))
         kernel = IQO_KERNEL_RYG;
     return kernel;
 }
@@ -1748,12 +1757,14 @@ int host_pipeline(HostStage *st, HostPlane *planes, int nPlanes)
     return IQO_HIP_OK;
 }
 
-// Large frames from pageable memory, the default: the HIP runtime's own pageable copies (it stages
-// through its pinned buffers at close to the PCIe rate: 44 GB/s H2D for a 12 MB plane set against
-// 53 GB/s from pinned memory, profiles/r05/pcie_probe.json), every plane's upload first, then the
-// kernels, then the downloads, one stream, one synchronisation.  Our own staging pipeline
-// (host_pipeline: pool memcpy into pinned memory + DMA per band) spent more host time on its per-band
-// copies, events and launches than the transfers take (C2 Y 0.43 ms, I420 0.58 ms).
+// Large frames, the default: whole-plane copies straight from the user's buffers (pageable ones
+// through the HIP runtime's own staging, which runs at close to the PCIe rate: 44 GB/s H2D for a
+// 12 MB plane set against 53 GB/s from pinned memory, profiles/r05/pcie_probe.json), every plane's
+// upload first, then the kernels, then the downloads, one stream, one synchronisation.  Our own
+// banded staging pipeline (host_pipeline: pool memcpy into pinned memory + DMA per band, option
+// host_stage = 1) spent more host time on its per-band copies, events and launches than the
+// transfers take: C2 Y 0.43 -> 0.24 ms from pageable memory, I420 0.58 -> 0.42 ms; from pinned
+// buffers the pipeline took 0.33 / 0.38 ms (profiles/r05/host_latency.txt).
 int host_direct(HostStage *st, HostPlane *planes, int nPlanes)
 {
     for (int q = 0; q < nPlanes; ++q) {
@@ -1835,7 +1846,7 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
         return IQO_HIP_OK;
     }
     HostPlane pl{h, srcSt, src, dstSt, dst, 0, 0, sPitch, dPitch, pinSrc, pinDst};
-    return h->hostStage || (pinSrc && pinDst) ? host_pipeline(st, &pl, 1) : host_direct(st, &pl, 1);
+    return h->hostStage ? host_pipeline(st, &pl, 1) : host_direct(st, &pl, 1);
 }
 
 int iqo_hip_resize(iqo_hip_plan *h, size_t srcSt, const uint8_t *src, size_t dstSt, uint8_t *dst)
@@ -2065,8 +2076,7 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
         HostPlane pl[3] = {{yp->y, srcStY, srcY, dstStY, dstY, 0, 0, sY, dY, pinY, pinYd},
                            {yp->c, srcStUV, srcU, dstStUV, dstU, oU, ou, sC, dC, pinU, pinUd},
                            {yp->c, srcStUV, srcV, dstStUV, dstV, oV, ov, sC, dC, pinV, pinVd}};
-        rc = yp->y->hostStage || (pinY && pinU && pinV && pinYd && pinUd && pinVd) ? host_pipeline(st, pl, 3)
-                                                                                    : host_direct(st, pl, 3);
+        rc = yp->y->hostStage ? host_pipeline(st, pl, 3) : host_direct(st, pl, 3);
     }
     if (rc) {
         (void)hipStreamSynchronize(st->sIn);

@@ -3730,9 +3730,10 @@ struct RygArgs {
     unsigned nBlocks;
 };
 
-template <bool LZ, int T, int NP, int PD>
+template <bool LZ, int T, int NP, int PD, int CPT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryg_kernel(RygArgs a)
 {
+    static_assert(CPT == 2 || CPT == 4, "output columns per thread");
     constexpr int OOB = 0x7ff00000;
     constexpr int PADB = 2 * kRyxPadK;  // work-row byte padding left of column 0
     static_assert(PD % 2 == 0 && T >= 2, "the unrolled trip covers both work-row buffers");
@@ -3771,12 +3772,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * span + 4 * k) = 0u;
     }
-    // the thread's output columns xLo + t and xLo + half + t (neighbouring lanes one column apart)
-    const int half = (xHi - xLo + 1) / 2;
-    int xc[2], aoff[2], sh[2], stoff[2];
-    uint32_t cf[2][NP], mm[2];
+    // the thread's output columns xLo + t + k half, k < CPT (neighbouring lanes one column apart)
+    const int half = (xHi - xLo + CPT - 1) / CPT;
+    int xc[CPT], aoff[CPT], sh[CPT], stoff[CPT];
+    uint32_t cf[CPT][NP], mm[CPT];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < CPT; ++k) {
         xc[k] = xLo + k * half + t;
         const int x = min(xc[k], xHi - 1);
         const int4 c = d.cols[x];
@@ -3788,7 +3789,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             cf[k][q] = d.colCoef[x * NP + q];
         stoff[k] = t < half && xc[k] < xHi ? xc[k] : OOB;
     }
-    const bool edgeT = LZ && (mm[0] != 0x80000000u || sh[0] != 19 || mm[1] != 0x80000000u || sh[1] != 19);
+    bool edgeAny = false;
+#pragma unroll
+    for (int k = 0; k < CPT; ++k)
+        edgeAny = edgeAny || mm[k] != 0x80000000u || sh[k] != 19;
+    const bool edgeT = LZ && edgeAny;
 
     auto load_row = [&](int r) -> uint32_t {
         const bool in = r >= rLo && r < rHi;
@@ -3859,9 +3864,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             const int s2 = rec_s(y + 2), c2 = rec_c(y + 2), sF = rec_s(y + 1 + PD);
             __syncthreads();
             const uint8_t *wr = lds + B * pitch;
-            uint32_t w[2][NP];
+            uint32_t w[CPT][NP];
 #pragma unroll
-            for (int k = 0; k < 2; ++k)
+            for (int k = 0; k < CPT; ++k)
 #pragma unroll
                 for (int q = 0; q < NP; ++q)
                     w[k][q] = reinterpret_cast<const uint32_t *>(wr + aoff[k])[q];
@@ -3892,28 +3897,33 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                 vertical(std::integral_constant<int, B ^ 1>{}, y + 1, cyn);
             nextS = s2;
             nextC = c2;
-            // horizontal: the thread's two columns of row y
-            uint32_t packed;
+            // horizontal: the thread's CPT columns of row y
+            uint32_t packed[CPT / 2];  // bytes of columns 2i, 2i + 1 in the low half
             if constexpr (LZ) {
-                int acc[2];
+                int acc[CPT];
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
+                for (int k = 0; k < CPT; ++k) {
                     acc[k] = sdot2_vv(w[k][0], cf[k][0], 1 << 19);
 #pragma unroll
                     for (int q = 1; q < NP; ++q)
                         acc[k] = sdot2(w[k][q], cf[k][q], acc[k]);
                 }
-                if (edgeT) {
-                    const uint32_t o0 = min(__umulhi(static_cast<uint32_t>(max(acc[0], 0)), mm[0]) >> sh[0], 255u);
-                    const uint32_t o1 = min(__umulhi(static_cast<uint32_t>(max(acc[1], 0)), mm[1]) >> sh[1], 255u);
-                    packed = opaque(o0) | (opaque(o1) << 8);
-                } else {
-                    packed = pack_lo(acc[0], acc[1]);  // sat_u8(acc >> 20) of both columns
+#pragma unroll
+                for (int i2 = 0; i2 < CPT / 2; ++i2) {
+                    if (edgeT) {
+                        const uint32_t o0 =
+                            min(__umulhi(static_cast<uint32_t>(max(acc[2 * i2], 0)), mm[2 * i2]) >> sh[2 * i2], 255u);
+                        const uint32_t o1 = min(
+                            __umulhi(static_cast<uint32_t>(max(acc[2 * i2 + 1], 0)), mm[2 * i2 + 1]) >> sh[2 * i2 + 1], 255u);
+                        packed[i2] = opaque(o0) | (opaque(o1) << 8);
+                    } else {
+                        packed[i2] = pack_lo(acc[2 * i2], acc[2 * i2 + 1]);  // sat_u8(acc >> 20) of both columns
+                    }
                 }
             } else {
-                int o[2];
+                int o[CPT];
 #pragma unroll
-                for (int k = 0; k < 2; ++k) {
+                for (int k = 0; k < CPT; ++k) {
                     uint32_t acc = 1u << 22;
 #pragma unroll
                     for (int q = 0; q < NP; ++q)
@@ -3921,11 +3931,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                     const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(acc) >> 23));
                     o[k] = u > 255 ? 255 : u;
                 }
-                packed = opaque(static_cast<uint32_t>(o[0])) | (opaque(static_cast<uint32_t>(o[1])) << 8);
+#pragma unroll
+                for (int i2 = 0; i2 < CPT / 2; ++i2)
+                    packed[i2] = opaque(static_cast<uint32_t>(o[2 * i2])) | (opaque(static_cast<uint32_t>(o[2 * i2 + 1])) << 8);
             }
             const int rowOff = (y - dstRow0) * dstSt;
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed), dstR, stoff[0] + rowOff, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed >> 8), dstR, stoff[1] + rowOff, 0, 0);
+#pragma unroll
+            for (int k = 0; k < CPT; ++k)
+                __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(packed[k / 2] >> (8 * (k & 1))), dstR,
+                                                     stoff[k] + rowOff, 0, 0);
         });
     }
 }
@@ -4933,17 +4947,18 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     // instantiations (plan.cpp build_ryg kShapes): taps, column pairs; PD = 4 output rows ahead
     struct Inst {
         bool lz;
-        int T, NP;
+        int T, NP, cpt;
         const void *kern;
     };
-#define IQO_RYG(LZ_, T_, NP_) {LZ_, T_, NP_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4>)}
+#define IQO_RYG(LZ_, T_, NP_)                                                                          \
+    {LZ_, T_, NP_, 2, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 2>)},              \
+    {LZ_, T_, NP_, 4, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 4>)}
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 6),
-                                 IQO_RYG(true, 12, 7),
-                                 IQO_RYG(false, 2, 2), IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3)};
+                                 IQO_RYG(true, 12, 7)};
 #undef IQO_RYG
     const void *kern = nullptr;
     for (const Inst &k : kInst)
-        if (k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP)
+        if (k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt)
             kern = k.kern;
     if (!kern || d.parts < 1 || d.parts > 16)
         return hipErrorInvalidValue;
@@ -4956,12 +4971,12 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
             return hipErrorInvalidValue;
         maxSpan = 0;
         for (int k = 0; k < d.parts; ++k) {
-            if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > 2 * threads || d.cs[k] % 4 ||
+            if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > d.cpt * threads || d.cs[k] % 4 ||
                 d.cs[k] < 0 || d.ce[k] > d.srcW || d.ce[k] - d.cs[k] > 4 * threads || d.ce[k] <= d.cs[k])
                 return hipErrorInvalidValue;
             maxSpan = std::max(maxSpan, d.ce[k] - d.cs[k]);
         }
-    } else if (d.srcW > 4 * threads || d.dstW > 2 * threads) {
+    } else if (d.srcW > 4 * threads || d.dstW > d.cpt * threads) {
         return hipErrorInvalidValue;
     }
     const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);

@@ -157,6 +157,7 @@ struct RygDev {
     const uint32_t *colCoef;
     int parts, threads;
     int xs[17], cs[16], ce[16];
+    int cpt;                     // output columns per thread: 2, or 4 on rows of more than 1024 outputs
 };
 hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

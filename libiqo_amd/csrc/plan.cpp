@@ -1543,7 +1543,7 @@ void build_ryg(const Plan &p, RyxTables *t)
     *t = RyxTables();
     // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart); widths
     // as ryx_kernel
-    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
+    if (p.method != kLanczos || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
         p.srcW < 16 || p.dstH < 4 || p.srcH <= p.dstH || p.srcH > 2 * p.dstH)
         return;
     const int T = p.y.taps;
@@ -1572,8 +1572,9 @@ void build_ryg(const Plan &p, RyxTables *t)
     struct Shape {
         int method, T, NP;
     };
-    static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5}, {kLanczos, 10, 6}, {kLanczos, 12, 7},
-                                    {kArea, 2, 2},    {kArea, 3, 2},    {kArea, 3, 3}};
+    // (Area: 2-3 taps, too little work per row for the per-row barrier; the wave walker is faster:
+    // 1080p -> 1366x768 x256 0.275 vs 0.348 ms, profiles/r05/steady_ryg.txt)
+    static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5}, {kLanczos, 10, 6}, {kLanczos, 12, 7}};
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
         if (S.method == p.method && S.T >= TE && S.T <= T && p.x.taps + 1 <= 2 * S.NP &&

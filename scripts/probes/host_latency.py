@@ -3,6 +3,7 @@ U/V 320x240 -> 160x120, Lanczos-2): plan construction, per-plane resize(), the 3
 Yuv420Resizer cycle with the constructor inside the loop (the reference benchmark's timed
 region, benchmark/benchmark.cpp:206-229).  Min / median microseconds over N repetitions."""
 import statistics
+import torch  # noqa: F401  (before libiqo_amd: torch initialises the HIP runtime first)
 import sys
 import time
 
