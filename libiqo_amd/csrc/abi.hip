@@ -1045,7 +1045,7 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // work per barrier (1080p -> 1366x768: 2 columns per thread took 4 parts of 256 threads)
     if (t.general && d.dstW > 1024) {
         d.cpt = 4;
-        if (split(2, 256) || split(1, 512) || split_min(512))
+        if ((h->ryxSplit != 0 && split(2, 256)) || split(1, 512) || split_min(512))  // ryx_split 0: one 8-wave part
             return d;
         d.cpt = 2;
         d.parts = 0;
