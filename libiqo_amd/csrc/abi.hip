@@ -50,11 +50,8 @@ struct iqo_hip_plan {
     int bands = 0;
     int debugFlags = 0;
     int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
-    int linPrefetch = 0;    // Linear 2x streamer: source rows in flight per wave (0 = default 2)
     int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
                             // streamer, 2: per-wave symmetric streamer (all bit-identical)
-    int xcdOrder = 1;       // block-shared streamer: XCD-aware workgroup order (speed only)
-    int ringPack = 0;       // block-shared streamer: ring rows packed (last DMA chunk masked)
     int rounds = 0;         // block-shared streamer: target rounds for the auto band count (0 = 6, -1 = makespan model)
     int tail = 0;           // block-shared streamer: short bands for each XCD's last frame (0 auto, -1 off, n bands)
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
@@ -63,7 +60,6 @@ struct iqo_hip_plan {
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
-    int ratioAlt = 1;       // 3:2, 3:1 and 2x kernels: odd row bands walk bottom-up (speed only)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
     // separable tile kernel (shapes without a specialised kernel; plan option "tile" = 0 turns
     // it off, leaving general_kernel)
@@ -621,10 +617,7 @@ void reset_options(iqo_hip_plan *h)
     h->bands = 0;
     h->debugFlags = 0;
     h->prefetch = 3;
-    h->linPrefetch = 0;
     h->streamVariant = 0;
-    h->xcdOrder = 1;
-    h->ringPack = 0;
     h->rounds = 0;
     h->tail = 0;
     h->stack = 1;
@@ -633,7 +626,6 @@ void reset_options(iqo_hip_plan *h)
     h->ryxCpt = 1;
     h->lanes = 0;
     h->ratioPrefetch = 0;
-    h->ratioAlt = 1;
     h->chunkFrames = 0;
     h->useTile = h->useWalk = h->useUp2 = h->useD32 = h->useD31 = h->useRyx = h->useL23 = h->useU23 = h->useA32 = true;
     h->useRyg = true;
@@ -791,7 +783,6 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.xNeg = f.xNeg;
     l.dbg = h->debugFlags;
     l.prefetch = h->prefetch;
-    l.ringPack = h->ringPack;
     l.rounds = h->rounds;
     l.tail = h->tail;
     l.stack = h->stack;
@@ -803,7 +794,6 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     for (int i = 0; i < f.NX / 2 && i < 10; ++i)
         (i < 8 ? l.cxo[i] : l.cy[i]) = pair16(f.cxo[2 * i], f.cxo[2 * i + 1]);  // (pairs 8, 9: Lanczos-5)
     l.np = h->lanes;
-    l.xcd = h->xcdOrder;
     return l;
 }
 
@@ -839,7 +829,6 @@ iqo_amd::LinearDev linear_dev(const iqo_hip_plan *h)
         l.cy[q] = pair16(p.fln.cy[q][0], p.fln.cy[q][1]);
     }
     l.dbg = h->debugFlags;
-    l.prefetch = h->linPrefetch;
     l.np = h->lanes;
     return l;
 }
@@ -898,7 +887,6 @@ iqo_amd::Up2Dev up2_dev(const iqo_hip_plan *h)
     d.F = u.F;
     d.NT = u.NT;
     d.np = h->lanes;
-    d.alt = h->ratioAlt;
     d.cy0 = u.cy0;
     d.cx0 = u.cx0;
     std::memcpy(d.cy1, u.cy1, sizeof d.cy1);
@@ -922,7 +910,6 @@ iqo_amd::D32Dev d32_dev(const iqo_hip_plan *h)
     d.dstH = h->p.dstH;
     d.np = h->lanes;
     d.pd = h->ratioPrefetch;
-    d.alt = h->ratioAlt;
     d.variant = t.variant;
     std::memcpy(d.cy, t.cy, sizeof d.cy);
     std::memcpy(d.cx, t.cx, sizeof d.cx);
@@ -945,7 +932,6 @@ iqo_amd::D31Dev d31_dev(const iqo_hip_plan *h)
     d.dstH = h->p.dstH;
     d.np = h->lanes;
     d.pd = h->ratioPrefetch;
-    d.alt = h->ratioAlt;
     d.variant = t.variant;
     d.cc = t.cc;
     std::memcpy(d.cp, t.cp, sizeof d.cp);
@@ -1506,24 +1492,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->stack = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "ring_pack")) {  // block-shared Lanczos streamer: packed ring rows (speed only)
-        h->ringPack = value != 0;
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "xcd_order")) {  // block-shared Lanczos streamer workgroup order (A/B)
-        h->xcdOrder = value != 0;
-        return IQO_HIP_OK;
-    }
     if (!std::strcmp(key, "prefetch")) {  // Lanczos streamer prefetch depth (rows)
         if (value < 1 || value > 4)
             return IQO_HIP_EINVAL;
         h->prefetch = static_cast<int>(value);
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "lin_prefetch")) {  // Linear 2x streamer: source rows in flight (2, 4, 8)
-        if (value != 0 && value != 2 && value != 4 && value != 8)
-            return IQO_HIP_EINVAL;
-        h->linPrefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stream_variant")) {  // A/B: 0 symmetric block-shared (default), 1 ring,
@@ -1569,10 +1541,6 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "a32")) {  // 0: exact 3:2 Area downscales use the wave walker alone
         h->useA32 = value != 0;
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "ratio_alt")) {  // 3:2 / 3:1 kernels: odd row bands walk bottom-up (speed only)
-        h->ratioAlt = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "ratio_prefetch")) {  // exact-ratio kernels: row groups loaded ahead (speed only);

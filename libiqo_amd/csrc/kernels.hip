@@ -593,7 +593,6 @@ struct LanczosArgs {
                              // (wrong output), 32 = all bands walk top-down.  0 in production.
     int np;                  // producing lanes per wave (symmetric streamer)
     int rowPitch, chunks;    // block-shared streamer: LDS ring row pitch, 1-KiB DMA chunks per row
-    int xcd;                 // block-shared streamer: XCD-aware workgroup order (xcd_spread)
     int lastLanes;           // block-shared streamer: lanes of the last DMA chunk (0 = all 64)
     int fpw, frames;         // frame-stacked streamer: frames per workgroup, frames in the launch
     // block-shared streamer, XCD tail split (tailBands > 0): XCD x takes frames [x F8, (x+1) F8),
@@ -1608,8 +1607,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 12 ? 2
             if (static_cast<int>(bx) >= a.tailBands)
                 return;
         }
-    } else if (a.xcd) {
-        // XCD-aware order (speed only): the band workgroups of one frame go to one XCD, so the
+    } else {
+        // XCD-aware order (speed only; plain dispatch order was 1 % slower, profiles/r05/steady_c2_final_opts.txt): the band workgroups of one frame go to one XCD, so the
         // halo rows two neighbouring bands share hit that XCD's L2, and each XCD streams from
         // 1/8 of the batch's address range
         const unsigned bands = gridDim.x;
@@ -2671,13 +2670,13 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
         const bool in = r >= 0 && r < u.srcH && r >= rFirst && r <= rLast;
         return __builtin_amdgcn_raw_buffer_load_b64(srcR, voff + (in ? (rc - srcRow0) * srcSt : OOB), 0, 0);
     };
-    // Odd bands walk bottom-up (u.alt; round 4, as lanczos_d32_kernel): the halo rows two
+    // Odd bands walk bottom-up (round 4, as lanczos_d32_kernel): the halo rows two
     // neighbouring bands share are then read by both at the same time, and the second read hits
     // L2.  Walk row t is source row rFirst + t top-down, rLast - t bottom-up; step j holds walk rows
     // j .. j + NT - 1 in both walks, so walking up, step j (k = kHi - 1 - j) finds tap i of the odd
     // output at walk row j + NT - 1 - i (the taps reversed: c1 below) and the even output's source
     // row k at walk row j + NT - 1 + OFF instead of j - OFF.
-    const bool up = u.alt && (band & 1);
+    const bool up = band & 1;
     const int wBase = up ? rLast : rFirst, wStep = up ? -1 : 1;
     auto walk_row = [&](int t) { return wBase + wStep * t; };
     uint32_t c1[F - 1][NT];  // phase 1 .. F-1 taps in walk order (SGPR selects, once per band)
@@ -2913,13 +2912,13 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
         return;
     const int kLo = yb >> 1;
     const int nG = (y1 - yb + 1) >> 1;  // groups of this band (dropped rows at either end)
-    // Odd bands walk bottom-up (d.alt): the halo rows two neighbouring bands share are then read
+    // Odd bands walk bottom-up: the halo rows two neighbouring bands share are then read
     // by both at the same time (both at their ends, or both at their starts) and the second read
     // hits L2 instead of HBM.  Walking up, relative row q is source row rLast - q and group g is
     // group kLo + nG - 1 - g; group row x of the forward walk is window row GW - 1 - x, so with
     // PO1 + NTY = GW the first output of a group (window rows 0 .. NTY-1) is the odd row with the
     // odd phase's taps reversed and the second (rows PO1 ..) the even row with the even taps reversed.
-    const bool up = d.alt && (band & 1);
+    const bool up = band & 1;
     const int mTop = kLo + nG - 1;
 
     const int opw = 8 * a.np;
@@ -3185,9 +3184,9 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
     if (y0 >= y1)
         return;
     const int nR = y1 - y0;
-    // odd bands walk bottom-up (d.alt; as lanczos_d32_kernel): the window is symmetric about its
+    // odd bands walk bottom-up (as lanczos_d32_kernel): the window is symmetric about its
     // centre row (2 CEN = NR - 1), so walking up is the same arithmetic on the rows in reverse
-    const bool up = d.alt && (band & 1);
+    const bool up = band & 1;
 
     const int opw = 4 * a.np;
     const int x0 = max(0, min(wcol * opw, d.dstW - opw));
@@ -5185,7 +5184,7 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     // 0.5226 vs 0.532 ms at depth 4), 4 -> 5.  Depth 5 packs the ring rows to the bytes they need
     // so that four 4-wave workgroups still fit a CU's LDS.
     const int K = pd <= 2 ? 3 : pd == 3 ? (l.NY >= 10 ? 5 : 4) : 5;
-    const bool pack = l.ringPack || (shared && K == 5);
+    const bool pack = shared && K == 5;
     const int rowPitch = pack ? rowNeed : 16 + 1024 * chunks;
     int fpw = 1;
     if (stack) {
@@ -5301,11 +5300,11 @@ hipError_t prep_lanczos(const LanczosDev &l, const Io &io, int rowBegin, int row
     const int rpb = (rows + bands - 1) / bands;
     bands = (rows + rpb - 1) / rpb;
     LanczosArgs &a = P->a;
-    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks, l.xcd,
+    a = LanczosArgs{l, io, rowBegin, rowEnd, rpb, 0, 0, bands, wpr, l.dbg, np, rowPitch, chunks,
                     pack ? lastLanes : 64, fpw, io.frames, 0, 0, 0};
     // XCD tail split: each XCD's last frame in short bands (about 8 rows; option "tail"), when
     // the batch splits evenly over the 8 XCDs into at least 2 frames each
-    if (shared && !stack && l.xcd && l.tail >= 0 && io.frames % 8 == 0 && io.frames >= 16) {
+    if (shared && !stack && l.tail >= 0 && io.frames % 8 == 0 && io.frames >= 16) {
         const int tb = l.tail > 0 ? min(l.tail, rows) : (rows + 7) / 8;
         const int tr = (rows + tb - 1) / tb;
         a.tailBands = (rows + tr - 1) / tr;
@@ -5402,14 +5401,11 @@ hipError_t prep_linear(const LinearDev &g, const Io &io, int rowBegin, int rowEn
     // nontemporal stores by default (variant builds: dbg 16 = plain stores, for A/B); 2 rows in
     // flight per wave measured best on C4 (the kernel is write-bound: 4 output bytes per source byte)
     const bool nt = g.F == 3 || !(IQO_DBG(g) & 16);
-    const int pd = g.prefetch == 0 || g.F == 3 ? 2 : g.prefetch;  // (3x: nontemporal, 2 ahead only)
-    const void *kern = g.F == 3  ? reinterpret_cast<const void *>(linear_up2_kernel<2, true, 3>)
-                       : pd >= 8 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<8, true, 2>)
-                                       : reinterpret_cast<const void *>(linear_up2_kernel<8, false, 2>))
-                       : pd >= 4 ? (nt ? reinterpret_cast<const void *>(linear_up2_kernel<4, true, 2>)
-                                       : reinterpret_cast<const void *>(linear_up2_kernel<4, false, 2>))
-                                 : (nt ? reinterpret_cast<const void *>(linear_up2_kernel<2, true, 2>)
-                                       : reinterpret_cast<const void *>(linear_up2_kernel<2, false, 2>));
+    // (round 2 also instantiated 4 and 8 rows in flight: no faster, removed in round 5)
+    const int pd = 2;
+    const void *kern = g.F == 3 ? reinterpret_cast<const void *>(linear_up2_kernel<2, true, 3>)
+                       : nt     ? reinterpret_cast<const void *>(linear_up2_kernel<2, true, 2>)
+                                : reinterpret_cast<const void *>(linear_up2_kernel<2, false, 2>);
     if (bands <= 0) {
         // ~6 rounds of resident waves, >= 16 rows per band (fresh data, C4 x256: 48 bands 0.537 ms
         // vs 0.555 for the one-round makespan choice)

@@ -79,7 +79,6 @@ struct Up2Dev {
     int m0, m1;                  // main rows; the others are masked border rows divided by
     uint32_t yM[2][16];          //   magic_y (top: row y, bottom: row y - m1)
     int yS[2][16];
-    int alt;                     // odd row bands walk bottom-up (speed only)
 };
 hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
@@ -89,7 +88,6 @@ struct D32Dev {
     int np;                      // producing lanes per wave (0 = auto)
     int pd;                      // row groups loaded ahead (1, 2, 4; 0 = default 1)
     int variant;                 // tap structure: 0 Lanczos-3 (10 taps), 1 Lanczos-2 (6 taps)
-    int alt;                     // odd row bands walk bottom-up (speed only)
     uint32_t cy[2][8];           // (c, c) u16 splats: phase p's taps at group rows 2p .. 2p + 7
     uint32_t cx[2][5];           // phase p's (c_2q, c_2q+1) int16 pairs
     uint32_t xM[2][8];           // edge-lane exact divisions (left / right 8 columns)
@@ -106,7 +104,6 @@ struct D31Dev {
     int np;                      // producing lanes per wave (0 = auto)
     int pd;                      // output rows loaded ahead (Lanczos-3: 1, 5; Lanczos-2: 1, 2, 4; 0 = 1)
     int variant;                 // tap structure: 0 Lanczos-3 (18 taps), 1 Lanczos-2 (12 taps)
-    int alt;                     // odd row bands walk bottom-up (speed only)
     uint32_t cc, cp[5];          // (c, c) u16 splats: the centre tap, the symmetric pairs' taps
     uint32_t cxe[9], cxo[9];     // (c_2q, c_2q+1) / (c_2q+1, c_2q+2) int16 pairs: even / odd window starts
     uint32_t xM[2][4];           // edge-lane exact divisions (left / right 4 columns)
@@ -216,8 +213,6 @@ struct LanczosDev {
     int NX, offXO;               // unpadded X taps, odd first tap column
     uint32_t cxo[8];             // (c_2p, c_2p+1) int16 pairs of the unpadded X table (Lanczos-5: below)
     int np;                      // producing lanes per wave (0 = auto)
-    int xcd;                     // block-shared streamer: XCD-aware workgroup order (speed only)
-    int ringPack;                // block-shared streamer: ring rows packed to the bytes they need
     int rounds;                  // block-shared streamer: target rounds of resident workgroups for the
                                  // auto band count (0 = default 6, -1 = one-round makespan model)
     int stack;                   // narrow frames: several frames per workgroup (lanczos_stack_kernel)
@@ -252,7 +247,6 @@ struct LinearDev {
     uint32_t cy[3];              // per phase (c0, c1) u16 pairs
     uint32_t cx[3];
     int dbg;                     // variant builds only: 16 = plain (not nontemporal) stores
-    int prefetch;                // source rows in flight per wave (2, 4, 8; 0 = default 2)
     int np;                      // producing lanes per wave (0 = auto)
 };
 hipError_t launch_linear_up2(const LinearDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
