@@ -3718,9 +3718,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
 // branch with register moves), and the incoming rows come from a FIFO of raw dwords loaded PD
 // output rows ahead -- always the last two rows of that row's window, so every output row issues
 // exactly two loads (branch-free memory stream, exact vmcnt waits; when the window moves by one row
-// the first of the two is the row the previous pair brought, an L2 hit).  Vertical: T packed MACs
-// per u16 pair; horizontal, LDS work rows, the next row's vertical pass under this row's LDS
-// reads, column tables and stores: as ryx_kernel with two output columns per thread.
+// the first of the two is the row the previous pair brought, an L2 hit).  The window is a RING of T
+// slots (round 5: fixed names shifted by register moves cost ~40 v_mov per row): window row k of
+// output y sits in slot (o(y) + k) mod T, o advancing with the window; one uniform switch on o picks
+// a copy of the row step with static slot names, which widens the two incoming rows into their
+// slots (when the window moves by one row the first lands on the equal row already there) and runs
+// the vertical pass.  Vertical: T packed MACs per u16 pair; horizontal, LDS work rows, the next
+// row's vertical pass under this row's LDS reads, column tables and stores: as ryx_kernel with CPT
+// output columns per thread.
 struct RygArgs {
     RygDev d;
     Io io;
@@ -3760,7 +3765,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     const __amdgpu_buffer_rsrc_t dstR = __builtin_amdgcn_make_buffer_rsrc(dstFrame, 0, a.dstBytes, 0x00020000);
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
-    const int rLo = max(0, srcRow0), rHi = min(d.srcH, a.io.srcRowEnd);  // loadable source rows
     const int span = cHi - cLo;
     const int voff = 4 * t < span ? cLo + 4 * t : OOB;
 
@@ -3794,17 +3798,19 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         edgeAny = edgeAny || mm[k] != 0x80000000u || sh[k] != 19;
     const bool edgeT = LZ && edgeAny;
 
+    // rows outside the window [srcRow0, srcRowEnd) load as zero: a row above it has a negative
+    // offset, one below it an offset past srcBytes, both outside the buffer range (no compares;
+    // prep_ryg checks that the offsets stay within 31 bits)
     auto load_row = [&](int r) -> uint32_t {
-        const bool in = r >= rLo && r < rHi;
-        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? (r - srcRow0) * srcSt : OOB), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (r - srcRow0) * srcSt, 0, 0);
     };
     auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
         W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
         W[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
     };
-    const int recLast = a.rowEnd - 1;
-    auto rec_s = [&](int y) { return sld(d.rowRec, 2 * min(y, recLast)); };
-    auto rec_c = [&](int y) { return sld(d.rowRec, 2 * min(y, recLast) + 1); };
+    // (plan.cpp build_ryg repeats the last record kRygRecPad >= PD + 2 times: no clamp)
+    auto rec_s = [&](int y) { return sld(d.rowRec, 2 * y); };
+    auto rec_c = [&](int y) { return sld(d.rowRec, 2 * y + 1); };
 
     // window of row y0, the FIFO (slot i: the last two window rows of row y0 + 1 + i)
     int curS = rec_s(y0);
@@ -3820,14 +3826,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         F[i][0] = load_row(use ? sF + T - 2 : -1);
         F[i][1] = load_row(use ? sF + T - 1 : -1);
     }
-    auto vertical = [&](auto bc, int y, const uint32_t (&cy)[T]) {
-        constexpr int B = decltype(bc)::value;
-        uint32_t W[2] = {0u, 0u};
+    // the row step with the window starting at ring slot O: incoming rows (raw dwords f0, f1:
+    // window rows T - 2, T - 1) widened into their slots when `fill`, then the packed MACs
+    auto ring_mac = [&](auto oc, bool fill, uint32_t f0, uint32_t f1, const uint32_t (&cy)[T], uint32_t (&W)[2]) {
+        constexpr int O = decltype(oc)::value;
+        if (fill) {
+            widen(f0, R[(O + T - 2) % T]);
+            widen(f1, R[(O + T - 1) % T]);
+        }
+        W[0] = 0u;
+        W[1] = 0u;
 #pragma unroll
         for (int k = 0; k < T; ++k) {
-            W[0] = pk_mad(R[k][0], cy[k], W[0]);
-            W[1] = pk_mad(R[k][1], cy[k], W[1]);
+            W[0] = pk_mad(R[(O + k) % T][0], cy[k], W[0]);
+            W[1] = pk_mad(R[(O + k) % T][1], cy[k], W[1]);
         }
+    };
+    auto vertical = [&](auto bc, int y, uint32_t (&W)[2]) {
+        constexpr int B = decltype(bc)::value;
         if (LZ && (y < d.m0 || y >= d.m1)) {
             // masked border row (uniform, rare): rows outside the image read as zero
             const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 15);
@@ -3838,13 +3854,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             *reinterpret_cast<uint2 *>(lds + B * pitch + PADB + 8 * t) = make_uint2(W[0], W[1]);
     };
     {
-        uint32_t cy0[T];
+        uint32_t cy0[T], W[2];
         const int co = rec_c(y0);
 #pragma unroll
         for (int k = 0; k < T; ++k)
             cy0[k] = static_cast<uint32_t>(sld(d.rowCoef, co + k));
-        vertical(std::integral_constant<int, 0>{}, y0, cy0);
+        ring_mac(std::integral_constant<int, 0>{}, false, 0u, 0u, cy0, W);
+        vertical(std::integral_constant<int, 0>{}, y0, W);
     }
+    int ro = 0;  // ring slot of the current window's first row
     int nextS = rec_s(y0 + 1), nextC = rec_c(y0 + 1);  // record of the next row, one row ahead
 
     for (int base = 0; base < nRows; base += PD) {
@@ -3869,31 +3887,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
                 for (int q = 0; q < NP; ++q)
                     w[k][q] = reinterpret_cast<const uint32_t *>(wr + aoff[k])[q];
-            if (more) {
-                // the next row's window (FIFO slot r), the slot's reload, its vertical pass
-                if (nextS - curS == 2) {
-#pragma unroll
-                    for (int k = 0; k < T - 2; ++k) {
-                        R[k][0] = R[k + 2][0];
-                        R[k][1] = R[k + 2][1];
-                    }
-                    widen(F[r][0], R[T - 2]);
-                    widen(F[r][1], R[T - 1]);
-                } else {
-#pragma unroll
-                    for (int k = 0; k < T - 1; ++k) {
-                        R[k][0] = R[k + 1][0];
-                        R[k][1] = R[k + 1][1];
-                    }
-                    widen(F[r][1], R[T - 1]);
-                }
-                curS = nextS;
-            }
+            // the FIFO slot's rows for the next row's window, the slot's reload, then the next row's
+            // ring step and vertical pass
+            const uint32_t f0 = F[r][0], f1 = F[r][1];
             const bool useF = i + 1 + PD < nRows;
             F[r][0] = load_row(useF ? sF + T - 2 : -1);
             F[r][1] = load_row(useF ? sF + T - 1 : -1);
-            if (more)
-                vertical(std::integral_constant<int, B ^ 1>{}, y + 1, cyn);
+            if (more) {
+                ro += nextS - curS;
+                ro = ro >= T ? ro - T : ro;
+                curS = nextS;
+                uint32_t W[2];
+                static_for<T>([&](auto oc) {
+                    if (ro == decltype(oc)::value)
+                        ring_mac(oc, true, f0, f1, cyn, W);
+                });
+                vertical(std::integral_constant<int, B ^ 1>{}, y + 1, W);
+            }
             nextS = s2;
             nextC = c2;
             // horizontal: the thread's CPT columns of row y
@@ -4952,8 +4962,8 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
 #define IQO_RYG(LZ_, T_, NP_)                                                                          \
     {LZ_, T_, NP_, 2, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 2>)},              \
     {LZ_, T_, NP_, 4, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 4>)}
-    static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 6),
-                                 IQO_RYG(true, 12, 7)};
+    static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
+                                 IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7)};
 #undef IQO_RYG
     const void *kern = nullptr;
     for (const Inst &k : kInst)

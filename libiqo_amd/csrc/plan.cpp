@@ -1390,6 +1390,7 @@ void build_d32(const Plan &p, const WalkTables &w, D32Tables *d)
 }
 
 bool ryx_columns(const Plan &p, int NP, RyxTables *t);
+int ryx_column_pairs(const Plan &p);
 
 void build_ryx(const Plan &p, RyxTables *t)
 {
@@ -1458,9 +1459,10 @@ void build_ryx(const Plan &p, RyxTables *t)
                                     {kLanczos, 2, 1, 16, 11}, {kLanczos, 2, 1, 18, 13}, {kLanczos, 2, 1, 20, 15},
                                     {kLanczos, 2, 1, 22, 17}, {kLanczos, 2, 1, 24, 19}, {kLanczos, 4, 9, 6, 4},
                                     {kLanczos, 4, 9, 4, 3}};
+    const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.P == P && S.Q == Q && S.T >= TE && S.T <= maxEnd - minOff && p.x.taps + 1 <= 2 * S.NP &&
+        if (S.method == p.method && S.P == P && S.Q == Q && S.T >= TE && S.T <= maxEnd - minOff && needNP <= S.NP &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))
             best = &S;
     if (!best)
@@ -1574,10 +1576,12 @@ void build_ryg(const Plan &p, RyxTables *t)
     };
     // (Area: 2-3 taps, too little work per row for the per-row barrier; the wave walker is faster:
     // 1080p -> 1366x768 x256 0.275 vs 0.348 ms, profiles/r05/steady_ryg.txt)
-    static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5}, {kLanczos, 10, 6}, {kLanczos, 12, 7}};
+    static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5},  {kLanczos, 10, 5},
+                                    {kLanczos, 10, 6}, {kLanczos, 12, 7}};
+    const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.T >= TE && S.T <= T && p.x.taps + 1 <= 2 * S.NP &&
+        if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))
             best = &S;
     if (!best)
@@ -1650,6 +1654,13 @@ void build_ryg(const Plan &p, RyxTables *t)
     }
     if (!ryx_columns(p, NP, t))
         return;
+    // kRygRecPad copies of the last record: the kernel reads the records of rows up to its prefetch
+    // depth + 2 past the band's end without clamping (their loads are masked)
+    const int32_t lastS = t->rowRec[static_cast<size_t>(2 * p.dstH - 2)], lastC = t->rowRec[static_cast<size_t>(2 * p.dstH - 1)];
+    for (int k = 0; k < kRygRecPad; ++k) {
+        t->rowRec.push_back(lastS);
+        t->rowRec.push_back(lastC);
+    }
     t->general = true;
     t->P = 0;
     t->Q = 0;
@@ -1661,9 +1672,37 @@ void build_ryg(const Plan &p, RyxTables *t)
     t->ok = true;
 }
 
-// The tabled columns of ryx_kernel / ryg_kernel: the reference's window, made to start on an even
-// column (a leading zero coefficient), NP pairs; masked Lanczos border taps outside the image meet
-// the zero padding of the work row
+// The nonzero taps [first, last] of output column x (round 5: the column tables drop the zero taps
+// at either end of a window, e.g. Lanczos-3 1920 -> 1366 has 10-tap windows holding at most 9
+// nonzero taps: 5 pairs instead of 6)
+static void column_nonzero(const Plan &p, int x, int *first, int *last)
+{
+    const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
+    const int32_t *c = &p.x.table[static_cast<size_t>(ci.tabOff)];
+    int a = 0, b = p.x.taps - 1;
+    while (a < b && c[a] == 0)
+        ++a;
+    while (b > a && c[b] == 0)
+        --b;
+    *first = a;
+    *last = b;
+}
+
+int ryx_column_pairs(const Plan &p)
+{
+    int need = 0;
+    for (int x = 0; x < p.dstW; ++x) {
+        int a, b;
+        column_nonzero(p, x, &a, &b);
+        const int start = p.x.coord[static_cast<size_t>(x)].srcO + a;
+        need = std::max(need, (start + (b - a) - (start & ~1)) / 2 + 1);
+    }
+    return need;
+}
+
+// The tabled columns of ryx_kernel / ryg_kernel: the reference's window less its zero end taps,
+// made to start on an even column (a leading zero coefficient), NP pairs; masked Lanczos border
+// taps outside the image meet the zero padding of the work row
 bool ryx_columns(const Plan &p, int NP, RyxTables *t)
 {
     t->cols.assign(static_cast<size_t>(p.dstW) * 4, 0);
@@ -1672,13 +1711,15 @@ bool ryx_columns(const Plan &p, int NP, RyxTables *t)
         const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
         if (ci.kind == kIdentity)
             return false;
-        const int start = ci.srcO;
+        int k0, k1;
+        column_nonzero(p, x, &k0, &k1);
+        const int start = ci.srcO + k0;
         const int a = start & ~1;  // even start (floor)
-        if (a < -kRyxPad || a + 2 * NP > p.srcW + kRyxPad)
+        if (a < -kRyxPad || a + 2 * NP > p.srcW + kRyxPad || start - a + (k1 - k0) >= 2 * NP)
             return false;
         std::vector<int32_t> c(static_cast<size_t>(2 * NP), 0);
-        for (int k = 0; k < p.x.taps; ++k)
-            c[static_cast<size_t>(start - a + k)] = p.x.table[static_cast<size_t>(ci.tabOff + k)];
+        for (int k = k0; k <= k1; ++k)
+            c[static_cast<size_t>(start - a + k - k0)] = p.x.table[static_cast<size_t>(ci.tabOff + k)];
         for (int q = 0; q < NP; ++q)
             t->colCoef[static_cast<size_t>(x) * NP + q] = (static_cast<uint32_t>(c[static_cast<size_t>(2 * q)]) & 0xffffu) |
                                                        (static_cast<uint32_t>(c[static_cast<size_t>(2 * q + 1)]) << 16);

@@ -273,6 +273,7 @@ struct RyxTables {
 };
 // Work-row padding (u16 entries) left of source column 0 in the kernel's LDS work row.
 constexpr int kRyxPad = 24;
+constexpr int kRygRecPad = 8;  // build_ryg: row records repeated past the last row (kernels.hip ryg_kernel)
 void build_ryx(const Plan &p, RyxTables *t);
 // The general-row variant of build_ryx (IQO_KERNEL_RYG): Lanczos and Area downscales whose rows
 // shrink by more than 1 and at most 2 (e.g. 1080 -> 768, 1080 -> 576) and that no exact-ratio
