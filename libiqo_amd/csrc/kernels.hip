@@ -3505,7 +3505,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
 #pragma unroll
     for (int k = 0; k < CPT; ++k)
         edgeAny = edgeAny || mm[k] != 0x80000000u || sh[k] != 19;
-    const bool edgeT = LZ && edgeAny;
+    // (wave-uniform: the exact division of a border column equals the saturating pack on an interior
+    // one, so a wave holding any border column takes it for all its lanes -- no divergent branch)
+    const bool edgeT = LZ && __builtin_amdgcn_ballot_w64(edgeAny) != 0;
     // one byte store per column (a wave stores 64 consecutive bytes per instruction)
     int stoff[CPT];
 #pragma unroll
@@ -3589,7 +3591,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
                 W[1] = pk_mad(R[(P * v + S0 + k) % NW][1], cy[k], W[1]);
             }
         }
-        if (LZ && (y < d.m0 || y >= d.m1)) {
+        if (LZ && static_cast<unsigned>(y - d.m0) >= static_cast<unsigned>(d.m1 - d.m0)) {
             // masked border row (uniform, rare): rows outside the image read as zero
             const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 15);
             W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
@@ -3796,7 +3798,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
     for (int k = 0; k < CPT; ++k)
         edgeAny = edgeAny || mm[k] != 0x80000000u || sh[k] != 19;
-    const bool edgeT = LZ && edgeAny;
+    // (wave-uniform: the exact division of a border column equals the saturating pack on an interior
+    // one, so a wave holding any border column takes it for all its lanes -- no divergent branch)
+    const bool edgeT = LZ && __builtin_amdgcn_ballot_w64(edgeAny) != 0;
 
     // rows outside the window [srcRow0, srcRowEnd) load as zero: a row above it has a negative
     // offset, one below it an offset past srcBytes, both outside the buffer range (no compares;
@@ -3844,7 +3848,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     };
     auto vertical = [&](auto bc, int y, uint32_t (&W)[2]) {
         constexpr int B = decltype(bc)::value;
-        if (LZ && (y < d.m0 || y >= d.m1)) {
+        if (LZ && static_cast<unsigned>(y - d.m0) >= static_cast<unsigned>(d.m1 - d.m0)) {
             // masked border row (uniform, rare): rows outside the image read as zero
             const int side = y < d.m0 ? 0 : 1, i = min(max(side ? y - d.m1 : y, 0), 15);
             W[0] = ydiv2(W[0], d.yM[side][i], d.yS[side][i]);
@@ -3898,6 +3902,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                 ro = ro >= T ? ro - T : ro;
                 curS = nextS;
                 uint32_t W[2];
+                // (a chain of uniform compares: a binary tree of them let the compiler turn the ring
+                // into a dynamically indexed scratch array)
                 static_for<T>([&](auto oc) {
                     if (ro == decltype(oc)::value)
                         ring_mac(oc, true, f0, f1, cyn, W);
@@ -4990,11 +4996,12 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     }
     const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
     const int rows = rowEnd - rowBegin;
-    // bands: ~2.5 rounds of resident workgroups, >= 16 rows each
+    // bands: ~6 rounds of resident workgroups, >= 32 rows each (steady clock, x256: 1080p -> 1366x768
+    // 12 bands 0.306 ms vs 5 bands 0.315, 1080p -> 1024x576 equal; profiles/r05/steady_ryg_bands.txt)
     if (bands <= 0) {
         const int64_t resident = std::max(1, resident_waves(kern, threads, ldsBytes) / (threads / 64));
         const int64_t perBand = static_cast<int64_t>(io.frames) * d.parts;
-        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
+        bands = static_cast<int>(std::min<int64_t>((6 * resident + perBand - 1) / perBand, std::max(1, rows / 32)));
     }
     bands = std::max(1, std::min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
