@@ -58,6 +58,7 @@ struct iqo_hip_plan {
     int ryxAdj = 1;         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
     int ryxCpt = 1;         // ratio-Y kernel: 4 output columns per thread at the Lanczos 4:9 upscales (speed only)
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
+    int rygCpt = 0;         // general-row kernel on rows of > 1024 outputs: output columns per thread (0 = auto)
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
@@ -622,6 +623,7 @@ void reset_options(iqo_hip_plan *h)
     h->tail = 0;
     h->stack = 1;
     h->ryxSplit = 1;
+    h->rygCpt = 0;
     h->ryxAdj = 1;
     h->ryxCpt = 1;
     h->lanes = 0;
@@ -1026,12 +1028,16 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
         d.cpt = 2;
         d.parts = 0;
     }
-    // general rows (ryg) on rows of more than 1024 outputs: 4 output columns per thread, so one
-    // workgroup per row (or per half row) does the row's vertical pass once and has 4 columns of
-    // work per barrier (1080p -> 1366x768: 2 columns per thread took 4 parts of 256 threads)
-    if (t.general && d.dstW > 1024) {
-        d.cpt = 4;
-        if ((h->ryxSplit != 0 && split(2, 256)) || split(1, 512) || split_min(512))  // ryx_split 0: one 8-wave part
+    // general rows (ryg): output columns per thread ~ 4 x dstW / srcW, so that the threads of the
+    // horizontal pass (CPT columns each) match those of the vertical pass (4 source columns each):
+    // 1080p -> 1366x768 with 3 columns per thread (two parts of 256 threads) 0.256 ms vs 4 columns
+    // 0.308 (a third of the threads idle in the horizontal pass), 2 columns needed four parts
+    // (profiles/r05/steady_ryg_cpt.txt); option "ryg_cpt" forces 2, 3 or 4
+    if (t.general) {
+        d.cpt = h->rygCpt ? h->rygCpt : std::min(4, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
+        const int tw = h->ryxSplit == 2 ? 128 : 64;
+        if ((h->ryxSplit >= 2 && split_min(tw)) || (h->ryxSplit == 1 && split(2, 256)) || split(1, 512) ||
+            split_min(512))  // (ryx_split 0: one 8-wave part where it fits)
             return d;
         d.cpt = 2;
         d.parts = 0;
@@ -1484,6 +1490,12 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 1)
             return IQO_HIP_EINVAL;
         h->ryxCpt = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryg_cpt")) {  // general-row kernel, rows of > 1024 outputs: columns per thread
+        if (value != 0 && (value < 2 || value > 4))  // (0 auto, 2, 3, 4; speed only)
+            return IQO_HIP_EINVAL;
+        h->rygCpt = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "stack")) {  // narrow frames side by side in one workgroup (speed only):

@@ -3739,7 +3739,8 @@ struct RygArgs {
 template <bool LZ, int T, int NP, int PD, int CPT>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryg_kernel(RygArgs a)
 {
-    static_assert(CPT == 2 || CPT == 4, "output columns per thread");
+    static_assert(CPT >= 2 && CPT <= 4, "output columns per thread");
+    constexpr int NPK = (CPT + 1) / 2;  // packed column pairs (an odd CPT: the last pair repeats its column)
     constexpr int OOB = 0x7ff00000;
     constexpr int PADB = 2 * kRyxPadK;  // work-row byte padding left of column 0
     static_assert(PD % 2 == 0 && T >= 2, "the unrolled trip covers both work-row buffers");
@@ -3913,7 +3914,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             nextS = s2;
             nextC = c2;
             // horizontal: the thread's CPT columns of row y
-            uint32_t packed[CPT / 2];  // bytes of columns 2i, 2i + 1 in the low half
+            uint32_t packed[NPK];  // bytes of columns 2i, 2i + 1 in the low half
             if constexpr (LZ) {
                 int acc[CPT];
 #pragma unroll
@@ -3924,15 +3925,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                         acc[k] = sdot2(w[k][q], cf[k][q], acc[k]);
                 }
 #pragma unroll
-                for (int i2 = 0; i2 < CPT / 2; ++i2) {
+                for (int i2 = 0; i2 < NPK; ++i2) {
+                    const int j0 = 2 * i2, j1 = min(2 * i2 + 1, CPT - 1);
                     if (edgeT) {
-                        const uint32_t o0 =
-                            min(__umulhi(static_cast<uint32_t>(max(acc[2 * i2], 0)), mm[2 * i2]) >> sh[2 * i2], 255u);
-                        const uint32_t o1 = min(
-                            __umulhi(static_cast<uint32_t>(max(acc[2 * i2 + 1], 0)), mm[2 * i2 + 1]) >> sh[2 * i2 + 1], 255u);
+                        const uint32_t o0 = min(__umulhi(static_cast<uint32_t>(max(acc[j0], 0)), mm[j0]) >> sh[j0], 255u);
+                        const uint32_t o1 = min(__umulhi(static_cast<uint32_t>(max(acc[j1], 0)), mm[j1]) >> sh[j1], 255u);
                         packed[i2] = opaque(o0) | (opaque(o1) << 8);
                     } else {
-                        packed[i2] = pack_lo(acc[2 * i2], acc[2 * i2 + 1]);  // sat_u8(acc >> 20) of both columns
+                        packed[i2] = pack_lo(acc[j0], acc[j1]);  // sat_u8(acc >> 20) of both columns
                     }
                 }
             } else {
@@ -3947,8 +3947,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                     o[k] = u > 255 ? 255 : u;
                 }
 #pragma unroll
-                for (int i2 = 0; i2 < CPT / 2; ++i2)
-                    packed[i2] = opaque(static_cast<uint32_t>(o[2 * i2])) | (opaque(static_cast<uint32_t>(o[2 * i2 + 1])) << 8);
+                for (int i2 = 0; i2 < NPK; ++i2)
+                    packed[i2] = opaque(static_cast<uint32_t>(o[2 * i2])) |
+                                 (opaque(static_cast<uint32_t>(o[min(2 * i2 + 1, CPT - 1)])) << 8);
             }
             const int rowOff = (y - dstRow0) * dstSt;
 #pragma unroll
@@ -4967,6 +4968,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     };
 #define IQO_RYG(LZ_, T_, NP_)                                                                          \
     {LZ_, T_, NP_, 2, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 2>)},              \
+    {LZ_, T_, NP_, 3, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 3>)},              \
     {LZ_, T_, NP_, 4, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 4>)}
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7)};
