@@ -59,6 +59,7 @@ struct iqo_hip_plan {
     int ryxCpt = 1;         // ratio-Y kernel: 4 output columns per thread at the Lanczos 4:9 upscales (speed only)
     int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
     int rygCpt = 0;         // general-row kernel on rows of > 1024 outputs: output columns per thread (0 = auto)
+    int ryxUc = 1;          // ratio-Y kernel: uniform column coefficients as scalars where every column has the same
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
     int ratioPrefetch = 0;  // exact-ratio kernels: row groups loaded ahead (0 = kernel default)
     int chunkFrames = 0;    // frames per launch (0 = up to 65535)
@@ -624,6 +625,7 @@ void reset_options(iqo_hip_plan *h)
     h->stack = 1;
     h->ryxSplit = 1;
     h->rygCpt = 0;
+    h->ryxUc = 1;
     h->ryxAdj = 1;
     h->ryxCpt = 1;
     h->lanes = 0;
@@ -1050,6 +1052,14 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // adjacent column pairs per thread (9:4 only, where every pair's windows start 1 or 2 pairs
     // apart, i.e. columns at 2:1 or more): one LDS run of NP + 2 dwords for both columns
     d.adj = 0;
+    if (d.parts > 0 && h->ryxAdj && d.P == 2 && d.Q == 1 && d.lanczos && d.cpt == 2) {
+        // 2:1 rows with 2:1 columns (uniform coefficients, below): every pair's windows one pair apart
+        bool ok = true;
+        for (int k = 0; k < d.parts && ok; ++k)
+            for (int x = d.xs[k]; x + 1 < d.xs[k + 1] && ok; x += 2)
+                ok = t.cols[static_cast<size_t>(x + 1) * 4] - t.cols[static_cast<size_t>(x) * 4] == 4;
+        d.adj = ok ? 1 : 0;
+    }
     if (d.parts > 0 && h->ryxAdj && d.P == 9 && d.Q == 4) {
         bool ok = true;
         for (int k = 0; k < d.parts && ok; ++k)
@@ -1059,6 +1069,20 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
             }
         d.adj = ok ? 1 : 0;
     }
+    // uniform column coefficients (Lanczos 2:1 columns): the kernel keeps them in scalar registers,
+    // not NP x CPT per-lane registers (Lanczos-9: 38 VGPRs, the difference between 2 and 4 waves
+    // per SIMD); option "ryx_uc" = 0 keeps the per-lane tables
+    d.uc = 0;
+    if (d.parts > 0 && h->ryxUc && d.lanczos && d.P == 2 && d.Q == 1 && d.cpt == 2) {
+        bool same = true;
+        const size_t np = static_cast<size_t>(t.NP);
+        for (size_t x = 1; x < static_cast<size_t>(d.dstW) && same; ++x)
+            same = std::equal(t.colCoef.begin() + static_cast<ptrdiff_t>(x * np), t.colCoef.begin() + static_cast<ptrdiff_t>((x + 1) * np),
+                              t.colCoef.begin());
+        d.uc = same ? 1 : 0;
+    }
+    if (d.adj && d.P == 2 && !d.uc)
+        d.adj = 0;  // (2:1 adjacent pairs: uniform-column instantiations only)
     return d;
 }
 
@@ -1490,6 +1514,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0 || value > 1)
             return IQO_HIP_EINVAL;
         h->ryxCpt = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryx_uc")) {  // ratio-Y kernel: 0 per-lane column coefficients everywhere (speed only)
+        h->ryxUc = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "ryg_cpt")) {  // general-row kernel, rows of > 1024 outputs: columns per thread

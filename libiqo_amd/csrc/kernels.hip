@@ -191,6 +191,17 @@ __device__ __forceinline__ void static_for(F &&f)
     static_for_impl(static_cast<F &&>(f), std::make_integer_sequence<int, N>{});
 }
 
+// Workgroup barrier that publishes this wave's LDS writes: an explicit lgkmcnt(0) before the
+// s_barrier.  (round 5: the compiler drops the wait of __syncthreads' release fence for LDS, and on
+// a loop back-edge no other wait preceded the barrier; the 2:1 ratio-Y kernel at 4K x128 then read
+// a neighbouring wave's outer taps stale now and then -- 1 to 100 pixels off by one per launch,
+// always at wave edges, profiles/r05/adj_race.txt)
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+    __syncthreads();
+}
+
 // ================================================================ general kernel
 
 enum { KMAIN = 0, KLO = 1, KHI = 2, KID = 3 };
@@ -309,11 +320,11 @@ __global__ __launch_bounds__(256) void general_kernel(GeneralArgs a)
         const int4 ch = a.g.chunks[c];
         for (int col = ch.z + static_cast<int>(threadIdx.x); col < ch.w; col += static_cast<int>(blockDim.x))
             wrow[col - ch.z] = y_value(a, srcF, yi, col);
-        __syncthreads();
+        lds_barrier();
         const int x = ch.x + static_cast<int>(threadIdx.x);
         if (x < ch.y)
             dstRow[x] = static_cast<uint8_t>(x_value(a, wrow, ch.z, ch.w, x));
-        __syncthreads();
+        lds_barrier();
     }
 }
 
@@ -466,7 +477,7 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
         for (int p = 0; p < NP; ++p)
             cf[k][p] = t.colCoef[(p * 4 + k) * t.nQp + Q];
     }
-    __syncthreads();
+    lds_barrier();
 
     // 1. vertical pass: tasks (row j, group g), g fastest; taps from the staged tile
     {
@@ -520,7 +531,7 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
             }
         }
     }
-    __syncthreads();
+    lds_barrier();
 
     // 2. horizontal pass
     const int dstSt = static_cast<int>(a.io.dstSt);
@@ -3380,14 +3391,21 @@ struct RyxArgs {
 #ifndef IQO_RYX_WPE
 #define IQO_RYX_WPE 4  // waves per SIMD the register budget is sized for (variant builds: 5)
 #endif
+#ifndef IQO_RYX_UC_PD
+#define IQO_RYX_UC_PD 2  // Lanczos-8 / -9 2:1 with uniform columns: row groups loaded ahead
+#endif
 #ifndef IQO_RYX_WPE_WIDE
 #define IQO_RYX_WPE_WIDE 2  // ... for windows of more than 20 rows: Lanczos-8 / -9 2:1 spill at 4 (steady clock, 4K 2:1
                             // x128: Lanczos-8 1.154 -> 0.533 ms, Lanczos-9 1.822 -> 0.567, profiles/r05/steady_check2.txt)
 #endif
-template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ, int CPT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQO_RYX_WPE_WIDE : IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
+template <bool LZ, int P, int Q, int T, int NP, int PD, bool ADJ, int CPT, bool UC = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !UC ? IQO_RYX_WPE_WIDE : IQO_RYX_WPE))) void ryx_kernel(RyxArgs a)
 {
     static_assert(CPT % 2 == 0 && (!ADJ || CPT == 2), "output columns per thread: pairs");
+    static_assert(!UC || !(P == 4 && Q == 1), "uniform columns: no rotated reads");
+    // adjacent pairs at 2:1 columns (round 5): the second column's window always starts one pair
+    // after the first's, so one run of NP + 1 pairs serves both (NP + 1 LDS dwords instead of 2 NP)
+    constexpr bool ADJ2 = ADJ && P == 2 && Q == 1;
     constexpr int SPAN = (P * (Q - 1)) / Q + T;   // window rows of one group of Q outputs
     constexpr int NW0 = (SPAN + P - 1) / P * P;   // register window rows (whole groups of P) ...
     constexpr int NW = ((NW0 / P) * Q) % 2 ? NW0 + P : NW0;  // ... and an even number of rows per trip
@@ -3458,7 +3476,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
 #pragma unroll
     for (int k = 0; k < CPT; ++k)
         xc[k] = ADJ ? xLo + 2 * t + k : xLo + k * half + t;
-    constexpr int NC1 = ADJ ? NP + 1 : NP;  // coefficient pairs of the second column
+    constexpr int NC1 = ADJ && !ADJ2 ? NP + 1 : NP;  // coefficient pairs of the second column
     uint32_t cf[CPT][NC1];
     int aoff[CPT];
     uint32_t mm[CPT];
@@ -3472,7 +3490,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
         sh[k] = c.z;
 #pragma unroll
         for (int q = 0; q < NP; ++q)
-            cf[k][q] = d.colCoef[x * NP + q];
+            cf[k][q] = UC ? static_cast<uint32_t>(sld(reinterpret_cast<const int *>(d.colCoef), q)) : d.colCoef[x * NP + q];
     }
     // 4:1: neighbouring lanes' windows are 2 dwords apart, so lanes t and t + 16 of a 32-lane half
     // meet on one bank (ds_read_b32 / ds_read2: bank = dword mod 32).  Lanes 16-31 of each half read
@@ -3492,7 +3510,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
         aoffB[k] = rot ? aoff[k] : aoff[k] + 4 * (NP - 1);
         aoff[k] += 4 * rot;
     }
-    if constexpr (ADJ) {
+    // ADJ2: reads start at the 8-byte boundary at or before the first column's window (base8);
+    // adjS = 1 when the window starts one dword after it (uniform: every 2:1 window has the same
+    // parity; lanes past xHi, clamped to the last column, may differ and store nothing)
+    const int base8 = ADJ2 ? aoff[0] & ~7 : 0;
+    const int adjS = ADJ2 ? (__builtin_amdgcn_readfirstlane(aoff[0]) >> 2) & 1 : 0;
+    uint32_t cfA[ADJ2 ? NP + 1 : 1];  // (uniform: scalar registers)
+    if constexpr (ADJ2) {
+#pragma unroll
+        for (int q = 0; q <= NP; ++q)
+            cfA[q] = adjS ? (q ? cf[0][q - 1] : 0u) : (q < NP ? cf[0][q] : 0u);
+    }
+    if constexpr (ADJ && !ADJ2) {  // (ADJ2: the second column's pairs are the first's, one pair later)
         const bool two = aoff[1] - aoff[0] == 8;  // else 4 (the pair's last thread past xHi: unused)
 #pragma unroll
         for (int q = NP; q >= 1; --q)
@@ -3626,12 +3655,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
             uint32_t cyn[TC];  // the next row's splats, complete at the barrier
             coefs(std::integral_constant<int, jn>{}, cyn);
             if (IQO_RYX_EXP != 3)  // experiment 3: no barrier (timing only)
-                __syncthreads();
+                lds_barrier();
             const uint8_t *wr = lds + B * pitch;
             // window pair q of column k: w[k][q] (ADJ: one run, the second column from pair 1)
-            constexpr int NR = ADJ ? NP + 2 : NP;
+            constexpr int NR = ADJ2 ? 2 * ((NP + 3) / 2) : ADJ ? NP + 2 : NP;
+            static_assert(!ADJ2 || NR >= NP + 2, "the run holds both columns' windows at either start");
             uint32_t w[ADJ ? 1 : CPT][NR];
-            if constexpr (ADJ) {
+            if constexpr (ADJ2) {
+                // 8-byte aligned ds_read_b64 from the pair boundary at or before the window: lanes
+                // 8 bytes apart, no bank conflicts (4-byte reads 2 dwords apart conflicted 2-way,
+                // and some lanes at wave edges then read stale outer taps, profiles/r05/adj_race.txt)
+                const uint2 *run = reinterpret_cast<const uint2 *>(__builtin_assume_aligned(wr + base8, 8));
+#pragma unroll
+                for (int q = 0; q < NR / 2; ++q) {
+                    const uint2 v = run[q];
+                    w[0][2 * q] = v.x;
+                    w[0][2 * q + 1] = v.y;
+                }
+            } else if constexpr (ADJ) {
 #pragma unroll
                 for (int q = 0; q < NR; ++q)
                     w[0][q] = reinterpret_cast<const uint32_t *>(wr + aoff[0])[q];
@@ -3644,6 +3685,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
                                              : *reinterpret_cast<const uint32_t *>(wr + aoffB[k]);
             }
             auto wq = [&](int k, int q) -> uint32_t { return ADJ ? w[0][k + q] : w[k][q]; };
+            // ADJ2: the two columns' sums over NP + 1 run pairs with the shifted coefficients cfA
+            // (column k's window starts at run pair k + adjS)
+            int acc2[2] = {0, 0};
+            if constexpr (ADJ2) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    acc2[k] = sdot2_vv(w[0][k], cfA[0], 1 << 19);
+#pragma unroll
+                    for (int q = 1; q <= NP; ++q)
+                        acc2[k] = sdot2(w[0][k + q], cfA[q], acc2[k]);
+                }
+            }
             // the next row's vertical pass (the next trip's first row after the trip's last)
             auto next_vertical = [&]() {
                 const int gn = base + (r + 1) / Q;
@@ -3663,6 +3716,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 ? IQ
                 int acc[CPT];
 #pragma unroll
                 for (int k = 0; k < CPT; ++k) {
+                    if constexpr (ADJ2) {
+                        acc[k] = acc2[k];
+                        continue;
+                    }
                     acc[k] = sdot2_vv(wq(k, 0), cf[k][0], 1 << 19);
 #pragma unroll
                     for (int q = 1; q < (k ? NC1 : NP); ++q)
@@ -3884,7 +3941,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             for (int k = 0; k < T; ++k)
                 cyn[k] = static_cast<uint32_t>(sld(d.rowCoef, nextC + k));
             const int s2 = rec_s(y + 2), c2 = rec_c(y + 2), sF = rec_s(y + 1 + PD);
-            __syncthreads();
+            lds_barrier();
             const uint8_t *wr = lds + B * pitch;
             uint32_t w[CPT][NP];
 #pragma unroll
@@ -4871,10 +4928,14 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         int P, Q, T, NP;
         bool adj;
         int cpt;
+        bool uc;  // uniform column coefficients (scalars)
         const void *kern;
     };
 #define IQO_RYX_C(LZ_, P_, Q_, T_, NP_, PD_, ADJ_, CPT_)                                                        \
-    {LZ_, P_, Q_, T_, NP_, ADJ_, CPT_, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_, ADJ_, CPT_>)}
+    {LZ_, P_, Q_, T_, NP_, ADJ_, CPT_, false, reinterpret_cast<const void *>(ryx_kernel<LZ_, P_, Q_, T_, NP_, PD_, ADJ_, CPT_>)}
+#define IQO_RYX_UA(P_, Q_, T_, NP_, PD_, ADJ_)                                                                \
+    {true, P_, Q_, T_, NP_, ADJ_, 2, true, reinterpret_cast<const void *>(ryx_kernel<true, P_, Q_, T_, NP_, PD_, ADJ_, 2, true>)}
+#define IQO_RYX_U(P_, Q_, T_, NP_, PD_) IQO_RYX_UA(P_, Q_, T_, NP_, PD_, false), IQO_RYX_UA(P_, Q_, T_, NP_, PD_, true)
 #define IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, ADJ_) IQO_RYX_C(LZ_, P_, Q_, T_, NP_, PD_, ADJ_, 2)
 #define IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_) IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, false)
 #define IQO_RYX2(LZ_, P_, Q_, T_, NP_, PD_) IQO_RYX(LZ_, P_, Q_, T_, NP_, PD_), IQO_RYX_A(LZ_, P_, Q_, T_, NP_, PD_, true)
@@ -4889,16 +4950,24 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         IQO_RYX(true, 2, 1, 22, 17, 2), IQO_RYX(true, 2, 1, 24, 19, 2), // Lanczos-8 / -9 2:1
         IQO_RYX(true, 4, 9, 6, 4, 2), IQO_RYX(true, 4, 9, 4, 3, 2),     // Lanczos-3 / -2 4:9 up (480 -> 1080 rows)
         IQO_RYX_C(true, 4, 9, 6, 4, 2, false, 4),
+        // Lanczos 2:1 columns (uniform coefficients): no per-lane coefficient registers; adjacent
+        // column pairs (ryx_dev d.uc, d.adj)
+        IQO_RYX_U(2, 1, 4, 3, 2), IQO_RYX_U(2, 1, 12, 9, 3), IQO_RYX_U(2, 1, 16, 11, 4), IQO_RYX_U(2, 1, 18, 13, 5), IQO_RYX_U(2, 1, 20, 15, 5),
+        IQO_RYX_U(2, 1, 22, 17, IQO_RYX_UC_PD), IQO_RYX_U(2, 1, 24, 19, IQO_RYX_UC_PD),
     };
+#undef IQO_RYX_U
+#undef IQO_RYX_UA
 #undef IQO_RYX2
 #undef IQO_RYX
 #undef IQO_RYX_A
 #undef IQO_RYX_C
     const void *kern = nullptr;
     int trip = 0;
+    bool kernUc = false;
     for (const Inst &k : kInst)
         if (k.lz == d.lanczos && k.P == d.P && k.Q == d.Q && k.T == d.taps && k.NP == d.NP && k.adj == (d.adj != 0) &&
-            k.cpt == d.cpt) {
+            k.cpt == d.cpt && (!k.uc || d.uc) && (!kern || (k.uc && !kernUc))) {  // (the uniform-column one first)
+            kernUc = k.uc;
             kern = k.kern;
             const int span = (k.P * (k.Q - 1)) / k.Q + k.T, nw0 = (span + k.P - 1) / k.P * k.P;
             const int nw = ((nw0 / k.P) * k.Q) % 2 ? nw0 + k.P : nw0;

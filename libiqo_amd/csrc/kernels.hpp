@@ -136,6 +136,9 @@ struct RyxDev {
     // (kernels.hip ryx_kernel ADJ); 0: columns i and half + i of the part
     int adj = 0;
     int cpt = 2;                 // output columns per thread (2; 4 at the Lanczos-3 4:9 upscale)
+    // 1: every column has the same coefficient pairs (Lanczos 2:1 columns: one phase, windows all
+    // starting on the same parity), so the kernel reads them once as scalars (kernels.hip UC)
+    int uc = 0;
 };
 hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
@@ -154,7 +157,7 @@ struct RygDev {
     const uint32_t *colCoef;
     int parts, threads;
     int xs[17], cs[16], ce[16];
-    int cpt;                     // output columns per thread: 2, or 4 on rows of more than 1024 outputs
+    int cpt;                     // output columns per thread: 2 .. 4 (abi.hip ryx_dev)
 };
 hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 
