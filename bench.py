@@ -17,7 +17,7 @@ process per GPU, plus the HBM roofline fraction of the kernel.
   separately from the compute steps.
 
 Inputs are synthetic uniform-random U8 frames generated before timing.  Image mode cycles through
-several distinct device batches, one per step (--rotate; auto: >= 2.5 GB per cycle): relaunching
+several distinct device batches, one per step (--rotate; auto: >= 3 batches and >= 2.5 GB per cycle): relaunching
 the SAME batch lets the 256 MiB Infinity Cache serve part of the reads (C2: ~15 % faster), which no
 real pipeline sees; that figure is reported separately as reuse_probe.  Rank 0 prints ONE JSON
 line.  The CPU baseline (rank 0, N=1 only) times the reference's own CPU path -- its public
@@ -337,8 +337,8 @@ def main():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the same-batch reuse probe (N=1)")
     ap.add_argument("--rotate", type=int, default=0,
-                    help="distinct device batches cycled through, one per step (0 = auto: >= 2.5 GB per cycle, "
-                         "10x the Infinity Cache, so no step re-reads the previous steps' data from it)")
+                    help="distinct device batches cycled through, one per step (0 = auto: >= 3 batches and >= 2.5 GB "
+                         "per cycle, 10x the Infinity Cache, so no step re-reads the previous steps' data from it)")
     ap.add_argument("--alt-frames", type=int, default=-1,
                     help="also time this many frames per launch (rotated batches; -1 = 256 for c2, 0 = off)")
     ap.add_argument("--force-general", action="store_true")
@@ -406,8 +406,12 @@ def main():
         out_px_step = float(frames) * dw * dh * world
         # every step resizes a batch the previous steps did not touch: the batches cycle with at
         # least 2.5 GB between two uses of one batch (a repeated launch over the same batch gets
-        # part of its reads from the 256 MiB Infinity Cache; real pipelines bring new frames)
-        rot = args.rotate or max(2, int(-(-2.5e9 // bytes_launch)))
+        # part of its reads from the 256 MiB Infinity Cache; real pipelines bring new frames).  At
+        # least 3 batches: a launch's time depends on where in HBM its batch landed (C2 x1024: 1.81
+        # to 1.91 ms from one batch to the next), and 2 large batches sampled fewer placements
+        # (the driver's command: 0.701-0.703 with 2, 0.712-0.714 with 3, alternated on one box,
+        # profiles/r05/rotate_placement.txt)
+        rot = args.rotate or max(3, int(-(-2.5e9 // bytes_launch)))
         src = torch.randint(0, 256, (rot, frames, sh, sw), dtype=torch.uint8, device=dev, generator=gen)
         dst = torch.empty((rot, frames, dh, dw), dtype=torch.uint8, device=dev)
         nstep = [0]
