@@ -43,9 +43,10 @@ CONFIGS = {
     # its GFX clock to ~1.5 GHz for ~10-20 ms after a streaming kernel starts (power management;
     # GRBM_GUI_ACTIVE per dispatch, profiles/r05/clock_transient.txt), and at 256 frames (0.5 ms per
     # launch) a run of 5 warmup + 20 timed steps sits inside that dip; at 1024 frames (1.9 ms) the
-    # warmup steps cover it.  Steady state per launch: 256 frames 0.494 ms (frac 0.672), 1024 frames
-    # 1.935 ms (0.686), 2048 frames 3.855 ms (0.688) (profiles/r05/steady_*.txt).  The line also
-    # carries 256 frames (the round-3/4 headline batch) as batch_alt.
+    # warmup steps cover it.  Steady state per launch with round 5's 12-row bands: 1024 frames 1.857 ms
+    # (frac 0.715), 256 frames 0.48 ms (0.69) (profiles/r05/steady_c2_final_opts.txt,
+    # bench_lines_steady.jsonl).  The line also carries 256 frames (the round-3/4 headline batch) as
+    # batch_alt.
     "c2": ("lanczos", 3, 3840, 2160, 1920, 1080, 1, 1024, "C2 Lanczos-3 U8 1ch 3840x2160->1920x1080"),
     "c3": ("area", 0, 7680, 4320, 1920, 1080, 1, 64, "C3 Area U8 1ch 7680x4320->1920x1080"),
     "c4": ("linear", 0, 1920, 1080, 3840, 2160, 1, 256, "C4 Linear U8 1ch 1920x1080->3840x2160"),
@@ -327,7 +328,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=-1,
+                    help="untimed warmup steps (default -1: enough steps for >= 150 ms of launches, at least 10, so "
+                         "the timed steps run after the GPU's post-start clock dip, profiles/r05/clock_transient.txt)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (band mode: global frames; 0 = default)")
     ap.add_argument("--shard", default="image", choices=["image", "band"])
@@ -454,6 +457,14 @@ def main():
             r.resize_band(frames, mine.r0, rows, mine.s0, sw, wins[b].stride(0), wins[b].data_ptr(), dw,
                           bands_out[b].stride(0), bands_out[b].data_ptr(), sp)
 
+    if args.warmup < 0:
+        # auto warmup: one untimed step sizes it (>= 150 ms of back-to-back launches, >= 10 steps)
+        ew0, ew1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ew0.record(stream)
+        step()
+        ew1.record(stream)
+        torch.cuda.synchronize(dev)
+        args.warmup = int(min(5000, max(10, -(-150.0 // max(ew0.elapsed_time(ew1), 1e-3)))))
     log("rank %d/%d %s shard=%s frames=%d kernel=%s warmup=%d steps=%d" % (rank, world, label, args.shard, frames,
                                                                         kernel, args.warmup, args.steps))
     for _ in range(args.warmup):
