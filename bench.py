@@ -458,13 +458,17 @@ def main():
                           bands_out[b].stride(0), bands_out[b].data_ptr(), sp)
 
     if args.warmup < 0:
-        # auto warmup: one untimed step sizes it (>= 150 ms of back-to-back launches, >= 10 steps)
+        # auto warmup: a cold step, then 3 timed ones size it (>= 150 ms of back-to-back launches,
+        # >= 10 steps; the 4 sizing steps are not counted)
+        step()
+        torch.cuda.synchronize(dev)
         ew0, ew1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ew0.record(stream)
-        step()
+        for _ in range(3):
+            step()
         ew1.record(stream)
         torch.cuda.synchronize(dev)
-        args.warmup = int(min(5000, max(10, -(-150.0 // max(ew0.elapsed_time(ew1), 1e-3)))))
+        args.warmup = int(min(5000, max(10, -(-150.0 // max(ew0.elapsed_time(ew1) / 3, 1e-3)))))
     log("rank %d/%d %s shard=%s frames=%d kernel=%s warmup=%d steps=%d" % (rank, world, label, args.shard, frames,
                                                                         kernel, args.warmup, args.steps))
     for _ in range(args.warmup):
