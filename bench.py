@@ -77,6 +77,7 @@ CONFIGS = {
     "w2": ("area", 0, 1920, 1080, 1366, 768, 1, 256, "W2 Area U8 1ch 1920x1080->1366x768"),
     "w3": ("lanczos", 2, 1920, 1080, 1024, 576, 1, 256, "W3 Lanczos-2 U8 1ch 1920x1080->1024x576"),
     "u1": ("lanczos", 3, 640, 480, 1920, 1080, 1, 256, "U1 Lanczos-3 U8 1ch 640x480->1920x1080"),
+    "u2": ("lanczos", 3, 1024, 576, 1920, 1080, 1, 256, "U2 Lanczos-3 U8 1ch 1024x576->1920x1080"),
 }
 
 

@@ -1112,6 +1112,7 @@ iqo_amd::RygDev ryg_dev(const iqo_hip_plan *h)
     std::memcpy(d.cs, x.cs, sizeof d.cs);
     std::memcpy(d.ce, x.ce, sizeof d.ce);
     d.cpt = x.cpt;
+    d.nl = h->ryx.rowLoads;
     return d;
 }
 

@@ -3793,10 +3793,11 @@ struct RygArgs {
     unsigned nBlocks;
 };
 
-template <bool LZ, int T, int NP, int PD, int CPT>
+template <bool LZ, int T, int NP, int PD, int CPT, int NL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryg_kernel(RygArgs a)
 {
     static_assert(CPT >= 2 && CPT <= 4, "output columns per thread");
+    static_assert(NL == 1 || NL == 2, "rows loaded per output row: 2 (downscales), 1 (upscales)");
     constexpr int NPK = (CPT + 1) / 2;  // packed column pairs (an odd CPT: the last pair repeats its column)
     constexpr int OOB = 0x7ff00000;
     constexpr int PADB = 2 * kRyxPadK;  // work-row byte padding left of column 0
@@ -3880,12 +3881,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
     for (int k = 0; k < T; ++k)
         widen(load_row(curS + k), R[k]);
-    uint32_t F[PD][2];
+    uint32_t F[PD][2];  // (NL = 1: slot [1] only)
 #pragma unroll
     for (int i = 0; i < PD; ++i) {
         const bool use = i + 1 < nRows;
         const int sF = rec_s(y0 + 1 + i);
-        F[i][0] = load_row(use ? sF + T - 2 : -1);
+        F[i][0] = NL == 2 ? load_row(use ? sF + T - 2 : -1) : 0u;
         F[i][1] = load_row(use ? sF + T - 1 : -1);
     }
     // the row step with the window starting at ring slot O: incoming rows (raw dwords f0, f1:
@@ -3893,7 +3894,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     auto ring_mac = [&](auto oc, bool fill, uint32_t f0, uint32_t f1, const uint32_t (&cy)[T], uint32_t (&W)[2]) {
         constexpr int O = decltype(oc)::value;
         if (fill) {
-            widen(f0, R[(O + T - 2) % T]);
+            if constexpr (NL == 2)
+                widen(f0, R[(O + T - 2) % T]);
             widen(f1, R[(O + T - 1) % T]);
         }
         W[0] = 0u;
@@ -3953,7 +3955,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             // ring step and vertical pass
             const uint32_t f0 = F[r][0], f1 = F[r][1];
             const bool useF = i + 1 + PD < nRows;
-            F[r][0] = load_row(useF ? sF + T - 2 : -1);
+            if constexpr (NL == 2)
+                F[r][0] = load_row(useF ? sF + T - 2 : -1);
             F[r][1] = load_row(useF ? sF + T - 1 : -1);
             if (more) {
                 ro += nextS - curS;
@@ -5032,19 +5035,23 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     // instantiations (plan.cpp build_ryg kShapes): taps, column pairs; PD = 4 output rows ahead
     struct Inst {
         bool lz;
-        int T, NP, cpt;
+        int T, NP, cpt, nl;
         const void *kern;
     };
-#define IQO_RYG(LZ_, T_, NP_)                                                                          \
-    {LZ_, T_, NP_, 2, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 2>)},              \
-    {LZ_, T_, NP_, 3, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 3>)},              \
-    {LZ_, T_, NP_, 4, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 4>)}
+#define IQO_RYG_N(LZ_, T_, NP_, NL_)                                                                   \
+    {LZ_, T_, NP_, 2, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 2, NL_>)},    \
+    {LZ_, T_, NP_, 3, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 3, NL_>)},    \
+    {LZ_, T_, NP_, 4, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 4, NL_>)}
+#define IQO_RYG(LZ_, T_, NP_) IQO_RYG_N(LZ_, T_, NP_, 2)
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
-                                 IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7)};
+                                 IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
+                                 // upscales (windows 0 or 1 rows apart: one new row per output row)
+                                 IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1)};
+#undef IQO_RYG_N
 #undef IQO_RYG
     const void *kern = nullptr;
     for (const Inst &k : kInst)
-        if (k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt)
+        if (k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt && k.nl == d.nl)
             kern = k.kern;
     if (!kern || d.parts < 1 || d.parts > 16)
         return hipErrorInvalidValue;

@@ -158,6 +158,8 @@ struct RygDev {
     int parts, threads;
     int xs[17], cs[16], ce[16];
     int cpt;                     // output columns per thread: 2 .. 4 (abi.hip ryx_dev)
+    int nl = 2;                  // rows loaded per output row: 2 (downscales, windows 1 or 2 rows apart),
+                                 // 1 (upscales, windows 0 or 1 rows apart)
 };
 hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s);
 

@@ -1543,11 +1543,12 @@ void build_ryx(const Plan &p, RyxTables *t)
 void build_ryg(const Plan &p, RyxTables *t)
 {
     *t = RyxTables();
-    // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart); widths
-    // as ryx_kernel
+    // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart), or
+    // grow (round 5: windows 0 or 1 rows apart, one new row per output row); widths as ryx_kernel
     if (p.method != kLanczos || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
-        p.srcW < 16 || p.dstH < 4 || p.srcH <= p.dstH || p.srcH > 2 * p.dstH)
+        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 2 * p.dstH)
         return;
+    const bool up = p.dstH > p.srcH;
     const int T = p.y.taps;
     // Lanczos: outer taps that are zero in every phase are dropped (as build_ryx)
     int lo = 0, hi = T - 1;
@@ -1581,8 +1582,8 @@ void build_ryg(const Plan &p, RyxTables *t)
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP &&
-            (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))
+        if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP && (!up || S.T <= 6) &&
+            (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;
     if (!best)
         return;
@@ -1615,7 +1616,7 @@ void build_ryg(const Plan &p, RyxTables *t)
         const int s0 = ci.srcO + off;
         if (y > 0) {
             const int adv = s0 - t->rowRec[static_cast<size_t>(2 * y - 2)];
-            if (adv < 1 || adv > 2)
+            if (adv < (up ? 0 : 1) || adv > (up ? 1 : 2))
                 return;
         }
         t->rowRec[static_cast<size_t>(2 * y)] = s0;
@@ -1662,6 +1663,7 @@ void build_ryg(const Plan &p, RyxTables *t)
         t->rowRec.push_back(lastC);
     }
     t->general = true;
+    t->rowLoads = up ? 1 : 2;
     t->P = 0;
     t->Q = 0;
     t->taps = TK;

@@ -269,6 +269,7 @@ struct RyxTables {
     // record {first window row, offset of its phase's taps in rowCoef} and consecutive windows
     // start 1 or 2 rows apart (downscales of 1 .. 2 : 1)
     bool general = false;
+    int rowLoads = 2;                      // general rows: 2 (downscale), 1 (upscale) new rows per output row
     std::vector<int32_t> rowRec;           // dstH x 2
 };
 // Work-row padding (u16 entries) left of source column 0 in the kernel's LDS work row.
