@@ -2835,9 +2835,14 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
             widen(pre[v], R[(v + NT - 1) % NW]);  // walk row j + NT - 1
             pre[v] = load_row(walk_row(j + NW + NT - 1));
             uint32_t Wk[4];
+            // output row F k: the source row k itself (both candidate rows through opaque(): a plain
+            // select of the two let the compiler index the window dynamically, i.e. put it in
+            // scratch -- 2 to 3x slower, round 5)
 #pragma unroll
-            for (int q = 0; q < 4; ++q)  // output row F k: the source row k itself
-                Wk[q] = pk_mul(up ? R[(v + NT - 1 + OFF) % NW][q] : R[(v - OFF) % NW][q], u.cy0);
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t ru = opaque(R[(v + NT - 1 + OFF) % NW][q]), rd = opaque(R[(v - OFF) % NW][q]);
+                Wk[q] = pk_mul(up ? ru : rd, u.cy0);
+            }
             border_row(Wk, F * k);
             emit(Wk, F * k, slot);
 #pragma unroll
