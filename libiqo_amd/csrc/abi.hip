@@ -1036,8 +1036,9 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // 0.308 (a third of the threads idle in the horizontal pass), 2 columns needed four parts
     // (profiles/r05/steady_ryg_cpt.txt); option "ryg_cpt" forces 2, 3 or 4
     if (t.general) {
-        d.cpt = h->rygCpt ? h->rygCpt : std::min(t.taps >= 12 ? 3 : 4, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
-        // (12-row windows with 4 columns per thread spill: 3 at most there)
+        d.cpt = h->rygCpt ? h->rygCpt
+                          : std::min(t.taps >= 12 || t.NP >= 6 ? 3 : 4, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
+        // (12-row windows or 6 column pairs with 4 columns per thread spill: 3 at most there)
         const int tw = h->ryxSplit == 2 ? 128 : 64;
         if ((h->ryxSplit >= 2 && split_min(tw)) || (h->ryxSplit == 1 && split(2, 256)) || split(1, 512) ||
             split_min(512))  // (ryx_split 0: one 8-wave part where it fits)
