@@ -114,8 +114,8 @@ int iqo_hip_plan_prepare(iqo_hip_plan *plan);
  * "stack" (0 / 1 / 2: narrow frames side by side in one workgroup off / where a frame fills at
  * most half a wave (default) / from two frames per workgroup), "rounds" (block-shared streamer
  * band count in rounds of resident workgroups, 0 = 6), "tail" (its XCD tail split), "prefetch",
- * "ratio_prefetch", "ryx_split", "ryx_adj", "ryx_cpt", "stream_variant", "lanes", "chunk_frames",
- * "host_stage" (A/B of kernel variants and schedules, see libiqo_amd/csrc/abi.hip; round 5 removed
+ * "ratio_prefetch", "ryx_split", "ryx_adj", "ryx_cpt", "ryx_uc", "ryg_cpt", "stream_variant", "lanes",
+ * "chunk_frames", "host_stage" (A/B of kernel variants and schedules, see libiqo_amd/csrc/abi.hip; round 5 removed
  * "lin_prefetch", "ratio_alt", "ring_pack" and "xcd_order", which no default used).  Every option changes speed only,
  * never the output bytes.  IQO_HIP_EINVAL for an unknown key or value. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);
