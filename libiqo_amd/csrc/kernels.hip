@@ -3597,7 +3597,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !
     // summed first (widened bytes: <= 510 per half, one v_add_u32 for both halves), then one packed
     // MAC per pair -- T / 2 MACs and T / 2 adds instead of T MACs; the low 16 bits of
     // c (a + b) are those of c a + c b, the reference's int16 wrap
-    constexpr bool SYMV = LZ && P == 2 && Q == 1;
+    constexpr bool SYMV = LZ && (P == 2 || P == 4) && Q == 1;  // (round 5: 4:1 too)
     constexpr int TC = SYMV ? T / 2 : T;  // row coefficients the pass reads
     static_assert(!SYMV || T % 2 == 0, "symmetric 2:1 windows have an even tap count");
     auto coefs = [&](auto jc, uint32_t (&cy)[TC]) {

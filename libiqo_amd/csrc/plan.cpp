@@ -1474,7 +1474,7 @@ void build_ryx(const Plan &p, RyxTables *t)
     int off = std::min(lowest, maxEnd - TK);
     // Lanczos 2:1 (symmetric window, below): a window wider than the nonzero taps is padded evenly
     // on both sides (an instantiation with more taps, picked for its column pairs)
-    if (p.method == kLanczos && P == 2 && Q == 1 && (TK - TE) % 2 == 0 && lowest - (TK - TE) / 2 >= minOff &&
+    if (p.method == kLanczos && (P == 2 || P == 4) && Q == 1 && (TK - TE) % 2 == 0 && lowest - (TK - TE) / 2 >= minOff &&
         lowest - (TK - TE) / 2 + TK <= maxEnd)
         off = lowest - (TK - TE) / 2;
     t->rowCoef.assign(static_cast<size_t>(Q * TK), 0u);
@@ -1492,7 +1492,7 @@ void build_ryx(const Plan &p, RyxTables *t)
     // Lanczos 2:1 (one phase): the kernel pair-sums mirrored window rows before the packed MAC
     // (kernels.hip ryx_kernel SYMV), so its window must be symmetric -- the reference's 2:1 tables
     // are, and the zero-tap trim is symmetric too; anything else takes the other kernels
-    if (p.method == kLanczos && P == 2 && Q == 1)
+    if (p.method == kLanczos && (P == 2 || P == 4) && Q == 1)
         for (int w = 0; w < TK; ++w)
             if (t->rowCoef[static_cast<size_t>(w)] != t->rowCoef[static_cast<size_t>(TK - 1 - w)])
                 return;
