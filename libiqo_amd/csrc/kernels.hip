@@ -5051,7 +5051,9 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
                                  // upscales (windows 0 or 1 rows apart: one new row per output row)
-                                 IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1)};
+                                 IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1),
+                                 // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)
+                                 IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3)};
 #undef IQO_RYG_N
 #undef IQO_RYG
     const void *kern = nullptr;

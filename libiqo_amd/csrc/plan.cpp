@@ -1545,10 +1545,12 @@ void build_ryg(const Plan &p, RyxTables *t)
     *t = RyxTables();
     // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart), or
     // grow (round 5: windows 0 or 1 rows apart, one new row per output row); widths as ryx_kernel
-    if (p.method != kLanczos || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
-        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 2 * p.dstH)
+    if ((p.method != kLanczos && p.method != kArea) || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 ||
+        p.srcW % 4 || p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 2 * p.dstH)
         return;
     const bool up = p.dstH > p.srcH;
+    if (up && p.method != kLanczos)
+        return;
     const int T = p.y.taps;
     // Lanczos: outer taps that are zero in every phase are dropped (as build_ryx)
     int lo = 0, hi = T - 1;
@@ -1575,10 +1577,11 @@ void build_ryg(const Plan &p, RyxTables *t)
     struct Shape {
         int method, T, NP;
     };
-    // (Area: 2-3 taps, too little work per row for the per-row barrier; the wave walker is faster:
-    // 1080p -> 1366x768 x256 0.275 vs 0.348 ms, profiles/r05/steady_ryg.txt)
+    // (Area, 3 taps: slower than the wave walker with the first ryg (1080p -> 1366x768 x256 0.348 vs
+    // 0.275 ms, profiles/r05/steady_ryg.txt), faster since the ring and the columns-per-thread rule:
+    // 0.199 vs 0.271 ms, profiles/r05/steady_ryg_area.txt)
     static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5},  {kLanczos, 10, 5},
-                                    {kLanczos, 10, 6}, {kLanczos, 12, 7}};
+                                    {kLanczos, 10, 6}, {kLanczos, 12, 7}, {kArea, 3, 2},    {kArea, 3, 3}};
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)

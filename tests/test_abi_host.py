@@ -105,7 +105,7 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-2
     (("lanczos", 4, 1920, 1080, 1280, 720, 1), "ryg"),             # 3:2 Lanczos-4: general rows (1 or 2 apart)
     (("lanczos", 3, 1920, 1080, 1366, 768, 1), "ryg"),             # rows 45:32
-    (("area", 0, 1920, 1080, 1366, 768, 1), "walk"),              # (Area: the walker beats ryg)
+    (("area", 0, 1920, 1080, 1366, 768, 1), "ryg"),               # Area general rows (round 5: ryg 0.20 vs walker 0.27 ms)
     (("lanczos", 2, 1920, 1080, 1024, 576, 1), "ryg"),             # rows 15:8
     (("lanczos", 3, 1920, 1080, 900, 500, 1), "tile"),             # rows shrink by more than 2 (> 1.9:1: tiles)
     (("lanczos", 3, 1280, 720, 1920, 1080, 1), "lanczos_u23"),    # exact 2:3 Lanczos-3 upscale
