@@ -86,7 +86,7 @@ struct iqo_hip_plan {
     iqo_amd::RyxTables ryx;
     uint32_t *dRyxRowCoef = nullptr, *dRyxColCoef = nullptr;
     int4 *dRyxCols = nullptr;
-    int2 *dRyxRowRec = nullptr;  // general-row tables (ryx.general: the ryg kernel)
+    int4 *dRyxRowRec = nullptr;  // general-row tables (ryx.general: the ryg kernel, kernels.hpp RygDev)
     bool useRyg = true;
     int hostStage = 0;  // host-pointer path, frames >= 4 MiB: 0 the runtime's own pageable copies, 1 our pinned
                         // staging pipeline (host_pipeline), for A/B
@@ -511,9 +511,11 @@ int upload_exact(iqo_hip_plan *h)
     if (h->ryx.ok && ryx_dev(h).parts == 0)
         h->ryx = iqo_amd::RyxTables();  // no column split fits the workgroup limits
     if (h->ryx.ok && h->ryx.general) {
-        std::vector<int2> rr(h->ryx.rowRec.size() / 2);
-        for (size_t i = 0; i < rr.size(); ++i)
-            rr[i] = make_int2(h->ryx.rowRec[2 * i], h->ryx.rowRec[2 * i + 1]);
+        std::vector<int4> rr(h->ryx.rowRec.size() / 2);
+        for (size_t i = 0; i < rr.size(); ++i) {
+            const size_t ia = std::min(rr.size() - 1, i + iqo_amd::kRygPD - 1);  // (rows past the end repeat)
+            rr[i] = make_int4(h->ryx.rowRec[2 * i], h->ryx.rowRec[2 * i + 1], h->ryx.rowRec[2 * ia], 0);
+        }
         const int rc2 = upload(h, &h->dRyxRowRec, rr.data(), rr.size());
         if (rc2)
             return rc2;

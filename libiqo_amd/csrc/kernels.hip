@@ -3877,8 +3877,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         W[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
     };
     // (plan.cpp build_ryg repeats the last record kRygRecPad >= PD + 2 times: no clamp)
-    auto rec_s = [&](int y) { return sld(d.rowRec, 2 * y); };
-    auto rec_c = [&](int y) { return sld(d.rowRec, 2 * y + 1); };
+    auto rec_s = [&](int y) { return sld(d.rowRec, 4 * y); };
+    auto rec_c = [&](int y) { return sld(d.rowRec, 4 * y + 1); };
+    static_assert(PD == kRygPD, "row records carry s(y + PD - 1) for the FIFO (abi.hip)");
 
     // window of row y0, the FIFO (slot i: the last two window rows of row y0 + 1 + i)
     int curS = rec_s(y0);
@@ -3947,7 +3948,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
             for (int k = 0; k < T; ++k)
                 cyn[k] = static_cast<uint32_t>(sld(d.rowCoef, nextC + k));
-            const int s2 = rec_s(y + 2), c2 = rec_c(y + 2), sF = rec_s(y + 1 + PD);
+            const int4 r2 = sload(d.rowRec + (y + 2));  // {s, c, s(y + 1 + PD), 0} of row y + 2: one s_load_dwordx4
+            const int s2 = r2.x, c2 = r2.y, sF = r2.z;
             lds_barrier();
             const uint8_t *wr = lds + B * pitch;
             uint32_t w[CPT][NP];

@@ -144,6 +144,7 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
 
 // General-row variant (plan.hpp build_ryg; kernels.hip ryg_kernel): ryx's tabled columns and column
 // parts, rows from a per-row record table instead of an exact P:Q.
+constexpr int kRygPD = 4;  // ryg_kernel: output rows loaded ahead (the instantiations' PD)
 struct RygDev {
     bool lanczos;
     int srcW, srcH, dstW, dstH;
@@ -151,7 +152,9 @@ struct RygDev {
     int m0, m1;                  // Lanczos main rows; the others are masked border rows (magic_y)
     uint32_t yM[2][16];
     int yS[2][16];
-    const int2 *rowRec;          // dstH x {first window row, offset of the row's taps in rowCoef}
+    // per output row y (dstH + padding): {first window row s(y), offset of the row's taps in rowCoef,
+    // s(y + kRygPD - 1), 0} -- the kernel fetches row y + 2's record with one scalar load per row
+    const int4 *rowRec;
     const uint32_t *rowCoef;     // phases x taps (c, c) splats
     const int4 *cols;            // as RyxDev
     const uint32_t *colCoef;
