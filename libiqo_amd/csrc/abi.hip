@@ -1273,7 +1273,7 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
     // exact vertical ratio, tabled columns: dword loads; 2-byte stores (1-byte stores when the
     // destination is not 2-byte aligned, launch_ryx)
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE || (kernel == IQO_KERNEL_GENERAL && !h->forceGeneral)) &&
-        aligned(src, 4, srcSt, srcFrameSt) && ryx_usable(h))
+        ryx_usable(h))  // (round 5: unaligned dword loads verified on gfx950, profiles/r05/unaligned_src.txt)
         kernel = IQO_KERNEL_RYX;
     if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && h->at.ok && h->useA32 &&
         aligned(src, 4, srcSt, srcFrameSt) && aligned(dst, 8, dstSt, dstFrameSt))
@@ -1286,7 +1286,8 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LINEAR_U23;
     // general rows last (dword loads, byte stores)
-    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) && aligned(src, 4, srcSt, srcFrameSt) && ryg_usable(h))
+    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) &&
+        ryg_usable(h))
         kernel = IQO_KERNEL_RYG;
     return kernel;
 }

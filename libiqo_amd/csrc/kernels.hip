@@ -3455,18 +3455,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !
                        // 3 no barriers
 #endif
     const int span = cHi - cLo;  // this workgroup's source columns [cLo, cHi), 4 per thread
-    const int voff = 4 * t < span && IQO_RYX_EXP != 1 ? cLo + 4 * t : OOB;
+    // a source width that is not a multiple of 4 (round 5): the thread straddling the row end loads
+    // the dword ending at the last column and shifts it down, so it never reads past the row and its
+    // columns past the end are zero (the masked border taps)
+    const int vsh = 4 * t < span ? max(0, cLo + 4 * t + 4 - d.srcW) : 0;
+    const int voff = 4 * t < span && IQO_RYX_EXP != 1 ? cLo + 4 * t - vsh : OOB;
     // upscales: waves with no source columns (480 threads over 160 source dwords) skip the
     // vertical pass and its loads (uniform per wave; not at the downscales, where every wave has
     // source columns and the branch costs Lanczos-3 4:1 its prefetch: 0.36 -> 0.82 ms)
     const bool srcWave = Q <= P || 256 * __builtin_amdgcn_readfirstlane(t >> 6) < span;
 
     // work rows: two buffers of (pad + span + pad) u16, zero padding written once
-    const int pitch = PADB + 2 * span + PADB;
+    const int spanA = (span + 3) & ~3;  // (the last thread's dword, zero past the row end)
+    const int pitch = PADB + 2 * spanA + PADB;
     for (int i = t; i < 2 * (PADB / 4); i += static_cast<int>(blockDim.x)) {
         const int buf = i / (PADB / 4), k = i % (PADB / 4);
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
-        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * span + 4 * k) = 0u;
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * spanA + 4 * k) = 0u;
     }
     // this thread's two output columns: table entries for the whole band
     // Thread t owns output columns xLo + t and xLo + half + t: neighbouring lanes read windows
@@ -3558,7 +3563,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !
     const int rowOff0 = (rBase - srcRow0) * srcSt;
     auto load_row = [&](int q) -> uint32_t {
         const bool in = static_cast<unsigned>(q - qLo) <= static_cast<unsigned>(qHi - qLo);
-        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? rowOff0 + q * srcSt : OOB), 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? rowOff0 + q * srcSt : OOB), 0, 0) >> (8 * vsh);
     };
     auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
         W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
@@ -3832,14 +3837,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     const int srcSt = static_cast<int>(a.io.srcSt), dstSt = static_cast<int>(a.io.dstSt);
     const int srcRow0 = a.io.srcRow0, dstRow0 = a.io.dstRow0;
     const int span = cHi - cLo;
-    const int voff = 4 * t < span ? cLo + 4 * t : OOB;
+    // (a source width that is not a multiple of 4: as ryx_kernel, the straddling thread's dword ends
+    // at the last column and is shifted down)
+    const int vsh = 4 * t < span ? max(0, cLo + 4 * t + 4 - d.srcW) : 0;
+    const int voff = 4 * t < span ? cLo + 4 * t - vsh : OOB;
 
     // work rows: two buffers of (pad + span + pad) u16, zero padding written once
-    const int pitch = PADB + 2 * span + PADB;
+    const int spanA = (span + 3) & ~3;  // (the last thread's dword, zero past the row end)
+    const int pitch = PADB + 2 * spanA + PADB;
     for (int i = t; i < 2 * (PADB / 4); i += static_cast<int>(blockDim.x)) {
         const int buf = i / (PADB / 4), k = i % (PADB / 4);
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
-        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * span + 4 * k) = 0u;
+        *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * spanA + 4 * k) = 0u;
     }
     // the thread's output columns xLo + t + k half, k < CPT (neighbouring lanes one column apart)
     const int half = (xHi - xLo + CPT - 1) / CPT;
@@ -3870,7 +3879,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     // offset, one below it an offset past srcBytes, both outside the buffer range (no compares;
     // prep_ryg checks that the offsets stay within 31 bits)
     auto load_row = [&](int r) -> uint32_t {
-        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (r - srcRow0) * srcSt, 0, 0);
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (r - srcRow0) * srcSt, 0, 0) >> (8 * vsh);
     };
     auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
         W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
@@ -4921,7 +4930,7 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    if (d.srcW % 4 || d.srcW > 8192 || d.dstW > 4096)
+    if (d.srcW < 16 || d.srcW > 8192 || d.dstW > 4096)
         return hipErrorInvalidValue;
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;  // stores are relative to dstRow0
@@ -5006,7 +5015,7 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
     } else if (d.srcW > 4 * threads || d.dstW > d.cpt * threads) {
         return hipErrorInvalidValue;
     }
-    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
+    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * ((maxSpan + 3) & ~3));
     const int groupBegin = rowBegin - rowBegin % d.Q;
     const int rows = rowEnd - groupBegin;
     // bands: ~2.5 rounds of resident workgroups, whole trips per band
@@ -5033,7 +5042,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
-    if (d.srcW % 4 || d.srcW > 8192 || d.dstW > 4096 || !d.rowRec)
+    if (d.srcW < 16 || d.srcW > 8192 || d.dstW > 4096 || !d.rowRec)
         return hipErrorInvalidValue;
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;
@@ -5081,7 +5090,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     } else if (d.srcW > 4 * threads || d.dstW > d.cpt * threads) {
         return hipErrorInvalidValue;
     }
-    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * maxSpan);
+    const int ldsBytes = 2 * (4 * kRyxPadK + 2 * ((maxSpan + 3) & ~3));
     const int rows = rowEnd - rowBegin;
     // bands: ~6 rounds of resident workgroups, >= 32 rows each (steady clock, x256: 1080p -> 1366x768
     // 12 bands 0.306 ms vs 5 bands 0.315, 1080p -> 1024x576 equal; profiles/r05/steady_ryg_bands.txt)

@@ -1397,8 +1397,8 @@ void build_ryx(const Plan &p, RyxTables *t)
     *t = RyxTables();
     // widths: launch_ryx's limits (up to 4 column parts of 512 threads; abi.cpp ryx_dev drops the
     // kernel when no split fits)
-    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW % 4 ||
-        p.srcW < 16 || p.dstH < 4)
+    if (p.method == kLinear || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW < 16 ||
+        p.dstH < 4)
         return;
     // the kernel's register window holds the rows of one group of Q outputs: downscales, and the
     // Lanczos 4:9 upscale (480 -> 1080 rows)
@@ -1546,7 +1546,7 @@ void build_ryg(const Plan &p, RyxTables *t)
     // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart), or
     // grow (round 5: windows 0 or 1 rows apart, one new row per output row); widths as ryx_kernel
     if ((p.method != kLanczos && p.method != kArea) || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 ||
-        p.srcW % 4 || p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 2 * p.dstH)
+        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 2 * p.dstH)
         return;
     const bool up = p.dstH > p.srcH;
     if (up && p.method != kLanczos)

@@ -101,7 +101,9 @@ def test_host_tables_match_oracle_random():
     (("area", 0, 7680, 4320, 1920, 1080, 1), "area_int"),
     (("linear", 0, 1920, 1080, 3840, 2160, 1), "linear_up2"),
     (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "lanczos_up2"),   # exact 2x Lanczos: register-window streamer
-    (("lanczos", 3, 1921, 1080, 3842, 2160, 1), "walk"),          # general ratios: wave walker
+    (("lanczos", 3, 1921, 1080, 3842, 2160, 1), "ryg"),           # 2x rows on an odd width (round 5: ryg reads
+                                                                  # rows that are not dword-aligned)
+    (("lanczos", 4, 1921, 1080, 3000, 2500, 1), "walk"),          # Lanczos-4 upscale (no ryg shape): wave walker
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-2
     (("lanczos", 4, 1920, 1080, 1280, 720, 1), "ryg"),             # 3:2 Lanczos-4: general rows (1 or 2 apart)
     (("lanczos", 3, 1920, 1080, 1366, 768, 1), "ryg"),             # rows 45:32
@@ -112,7 +114,7 @@ def test_host_tables_match_oracle_random():
     (("linear", 0, 1280, 720, 1920, 1080, 1), "linear_u23"),      # exact 2:3 Linear upscale
     (("area", 0, 1920, 1080, 1280, 720, 1), "area_d32"),          # exact 3:2 Area: no window, no halo
     (("lanczos", 3, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-3: register window
-    (("area", 0, 1921, 1080, 1280, 720, 1), "walk"),
+    (("area", 0, 1921, 1080, 1280, 720, 1), "ryg"),              # (odd width: ryg since round 5)
     (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),
     (("lanczos", 3, 13, 9, 5, 40, 1), "tile"),                    # 13 columns: no 256-column strip fits the walker's tables
     (("lanczos", 9, 64, 48, 1000, 900, 1), "tile"),               # 64 work columns per row window: tiles
