@@ -3807,7 +3807,7 @@ template <bool LZ, int T, int NP, int PD, int CPT, int NL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryg_kernel(RygArgs a)
 {
     static_assert(CPT >= 2 && CPT <= 4, "output columns per thread");
-    static_assert(NL == 1 || NL == 2, "rows loaded per output row: 2 (downscales), 1 (upscales)");
+    static_assert(NL >= 1 && NL <= 3, "rows loaded per output row: 1 (upscales), 2 (down to 2:1), 3 (down to 3:1)");
     constexpr int NPK = (CPT + 1) / 2;  // packed column pairs (an odd CPT: the last pair repeats its column)
     constexpr int OOB = 0x7ff00000;
     constexpr int PADB = 2 * kRyxPadK;  // work-row byte padding left of column 0
@@ -3896,22 +3896,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
     for (int k = 0; k < T; ++k)
         widen(load_row(curS + k), R[k]);
-    uint32_t F[PD][2];  // (NL = 1: slot [1] only)
+    uint32_t F[PD][NL];  // slot i: window rows T - NL .. T - 1 of row y0 + 1 + i
 #pragma unroll
     for (int i = 0; i < PD; ++i) {
         const bool use = i + 1 < nRows;
         const int sF = rec_s(y0 + 1 + i);
-        F[i][0] = NL == 2 ? load_row(use ? sF + T - 2 : -1) : 0u;
-        F[i][1] = load_row(use ? sF + T - 1 : -1);
+#pragma unroll
+        for (int l = 0; l < NL; ++l)
+            F[i][l] = load_row(use ? sF + T - NL + l : -1);
     }
-    // the row step with the window starting at ring slot O: incoming rows (raw dwords f0, f1:
-    // window rows T - 2, T - 1) widened into their slots when `fill`, then the packed MACs
-    auto ring_mac = [&](auto oc, bool fill, uint32_t f0, uint32_t f1, const uint32_t (&cy)[T], uint32_t (&W)[2]) {
+    // the row step with the window starting at ring slot O: incoming rows (raw dwords f: window
+    // rows T - NL .. T - 1) widened into their slots when `fill`, then the packed MACs
+    auto ring_mac = [&](auto oc, bool fill, const uint32_t (&f)[NL], const uint32_t (&cy)[T], uint32_t (&W)[2]) {
         constexpr int O = decltype(oc)::value;
         if (fill) {
-            if constexpr (NL == 2)
-                widen(f0, R[(O + T - 2) % T]);
-            widen(f1, R[(O + T - 1) % T]);
+#pragma unroll
+            for (int l = 0; l < NL; ++l)
+                widen(f[l], R[(O + T - NL + l) % T]);
         }
         W[0] = 0u;
         W[1] = 0u;
@@ -3938,7 +3939,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 #pragma unroll
         for (int k = 0; k < T; ++k)
             cy0[k] = static_cast<uint32_t>(sld(d.rowCoef, co + k));
-        ring_mac(std::integral_constant<int, 0>{}, false, 0u, 0u, cy0, W);
+        const uint32_t none[NL] = {};
+        ring_mac(std::integral_constant<int, 0>{}, false, none, cy0, W);
         vertical(std::integral_constant<int, 0>{}, y0, W);
     }
     int ro = 0;  // ring slot of the current window's first row
@@ -3969,11 +3971,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                     w[k][q] = reinterpret_cast<const uint32_t *>(wr + aoff[k])[q];
             // the FIFO slot's rows for the next row's window, the slot's reload, then the next row's
             // ring step and vertical pass
-            const uint32_t f0 = F[r][0], f1 = F[r][1];
+            uint32_t f[NL];
+#pragma unroll
+            for (int l = 0; l < NL; ++l)
+                f[l] = F[r][l];
             const bool useF = i + 1 + PD < nRows;
-            if constexpr (NL == 2)
-                F[r][0] = load_row(useF ? sF + T - 2 : -1);
-            F[r][1] = load_row(useF ? sF + T - 1 : -1);
+#pragma unroll
+            for (int l = 0; l < NL; ++l)
+                F[r][l] = load_row(useF ? sF + T - NL + l : -1);
             if (more) {
                 ro += nextS - curS;
                 ro = ro >= T ? ro - T : ro;
@@ -3983,7 +3988,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
                 // into a dynamically indexed scratch array)
                 static_for<T>([&](auto oc) {
                     if (ro == decltype(oc)::value)
-                        ring_mac(oc, true, f0, f1, cyn, W);
+                        ring_mac(oc, true, f, cyn, W);
                 });
                 vertical(std::integral_constant<int, B ^ 1>{}, y + 1, W);
             }
@@ -5038,16 +5043,23 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
                            static_cast<size_t>(ldsBytes), s);
 }
 
+static hipError_t iqo_ryg_einval(int where)
+{
+    if (getenv("IQO_DEBUG_LAUNCH"))
+        fprintf(stderr, "launch_ryg: invalid argument at check %d\n", where);
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, int bands, hipStream_t s)
 {
     if (rowEnd <= rowBegin || io.frames <= 0)
         return hipSuccess;
     if (d.srcW < 16 || d.srcW > 8192 || d.dstW > 4096 || !d.rowRec)
-        return hipErrorInvalidValue;
+        return iqo_ryg_einval(1);
     const int64_t sb = static_cast<int64_t>(io.srcRowEnd - io.srcRow0 - 1) * io.srcSt + d.srcW;
     const int64_t db = static_cast<int64_t>(rowEnd - 1 - io.dstRow0) * io.dstSt + d.dstW;
     if (sb >= 0x7ff00000 || db >= 0x7ff00000 || io.srcSt >= (int64_t(1) << 24) || io.dstSt >= (int64_t(1) << 24))
-        return hipErrorInvalidValue;
+        return iqo_ryg_einval(2);
     // instantiations (plan.cpp build_ryg kShapes): taps, column pairs; PD = 4 output rows ahead
     struct Inst {
         bool lz;
@@ -5064,7 +5076,13 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  // upscales (windows 0 or 1 rows apart: one new row per output row)
                                  IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1),
                                  // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)
-                                 IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3)};
+                                 IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3),
+                                 // Lanczos downscales of 2 .. 3 : 1 (windows 2 or 3 rows apart; 2 columns per thread)
+                                 {true, 10, 6, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 10, 6, 4, 2, 3>)},
+                                 {true, 12, 7, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 12, 7, 4, 2, 3>)},
+                                 {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, 4, 2, 3>)},
+                                 {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, 4, 2, 3>)},
+                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 3>)}};
 #undef IQO_RYG_N
 #undef IQO_RYG
     const void *kern = nullptr;
@@ -5072,23 +5090,23 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
         if (k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt && k.nl == d.nl)
             kern = k.kern;
     if (!kern || d.parts < 1 || d.parts > 16)
-        return hipErrorInvalidValue;
+        return iqo_ryg_einval(3);
     const int threads = d.threads > 0 ? d.threads : 512;
     if (threads % 64 || threads > 512)
-        return hipErrorInvalidValue;
+        return iqo_ryg_einval(4);
     int maxSpan = d.srcW;
     if (d.parts > 1) {
         if (d.xs[0] != 0 || d.xs[d.parts] != d.dstW)
-            return hipErrorInvalidValue;
+            return iqo_ryg_einval(5);
         maxSpan = 0;
         for (int k = 0; k < d.parts; ++k) {
             if (d.xs[k] % 2 || d.xs[k + 1] < d.xs[k] || d.xs[k + 1] - d.xs[k] > d.cpt * threads || d.cs[k] % 4 ||
                 d.cs[k] < 0 || d.ce[k] > d.srcW || d.ce[k] - d.cs[k] > 4 * threads || d.ce[k] <= d.cs[k])
-                return hipErrorInvalidValue;
+                return iqo_ryg_einval(6);
             maxSpan = std::max(maxSpan, d.ce[k] - d.cs[k]);
         }
     } else if (d.srcW > 4 * threads || d.dstW > d.cpt * threads) {
-        return hipErrorInvalidValue;
+        return iqo_ryg_einval(7);
     }
     const int ldsBytes = 2 * (4 * kRyxPadK + 2 * ((maxSpan + 3) & ~3));
     const int rows = rowEnd - rowBegin;
@@ -5104,7 +5122,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     bands = (rows + rpb - 1) / rpb;
     const uint64_t nBlocks = static_cast<uint64_t>(bands) * static_cast<uint64_t>(io.frames) * static_cast<uint64_t>(d.parts);
     if (nBlocks >= (uint64_t(1) << 31))
-        return hipErrorInvalidValue;
+        return iqo_ryg_einval(8);
     RygArgs a{d, io, rowBegin, rowEnd, rpb, bands, static_cast<int>(sb), static_cast<int>(db),
               static_cast<unsigned>(nBlocks)};
     void *args[] = {&a};

@@ -1546,9 +1546,12 @@ void build_ryg(const Plan &p, RyxTables *t)
     // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart), or
     // grow (round 5: windows 0 or 1 rows apart, one new row per output row); widths as ryx_kernel
     if ((p.method != kLanczos && p.method != kArea) || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 ||
-        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 2 * p.dstH)
+        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 3 * p.dstH)
         return;
     const bool up = p.dstH > p.srcH;
+    const int maxAdv = up ? 1 : p.srcH > 2 * p.dstH ? 3 : 2;  // window advance per output row (rows loaded)
+    if (maxAdv == 3 && p.method != kLanczos)
+        return;
     if (up && p.method != kLanczos)
         return;
     const int T = p.y.taps;
@@ -1580,12 +1583,14 @@ void build_ryg(const Plan &p, RyxTables *t)
     // (Area, 3 taps: slower than the wave walker with the first ryg (1080p -> 1366x768 x256 0.348 vs
     // 0.275 ms, profiles/r05/steady_ryg.txt), faster since the ring and the columns-per-thread rule:
     // 0.199 vs 0.271 ms, profiles/r05/steady_ryg_area.txt)
-    static const Shape kShapes[] = {{kLanczos, 4, 3}, {kLanczos, 6, 4}, {kLanczos, 8, 5},  {kLanczos, 10, 5},
-                                    {kLanczos, 10, 6}, {kLanczos, 12, 7}, {kArea, 3, 2},    {kArea, 3, 3}};
+    static const Shape kShapes[] = {{kLanczos, 4, 3},  {kLanczos, 6, 4},  {kLanczos, 8, 5},  {kLanczos, 10, 5},
+                                    {kLanczos, 10, 6}, {kLanczos, 12, 7}, {kArea, 3, 2},     {kArea, 3, 3},
+                                    {kLanczos, 14, 8}, {kLanczos, 16, 9}, {kLanczos, 18, 10}};
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
         if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP && (!up || S.T <= 6) &&
+            (maxAdv == 3 ? S.T >= 10 && S.NP == S.T / 2 + 1 : S.T <= 12) &&  // (kernels.hip: NL = 3 shapes (T, T/2 + 1), T 10 .. 18)
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;
     if (!best)
@@ -1619,7 +1624,7 @@ void build_ryg(const Plan &p, RyxTables *t)
         const int s0 = ci.srcO + off;
         if (y > 0) {
             const int adv = s0 - t->rowRec[static_cast<size_t>(2 * y - 2)];
-            if (adv < (up ? 0 : 1) || adv > (up ? 1 : 2))
+            if (adv < (up ? 0 : maxAdv - 1) || adv > maxAdv)
                 return;
         }
         t->rowRec[static_cast<size_t>(2 * y)] = s0;
@@ -1666,7 +1671,7 @@ void build_ryg(const Plan &p, RyxTables *t)
         t->rowRec.push_back(lastC);
     }
     t->general = true;
-    t->rowLoads = up ? 1 : 2;
+    t->rowLoads = maxAdv;
     t->P = 0;
     t->Q = 0;
     t->taps = TK;
