@@ -5074,7 +5074,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
                                  // upscales (windows 0 or 1 rows apart: one new row per output row)
-                                 IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1),
+                                 IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1), IQO_RYG_N(true, 8, 5, 1),
                                  // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)
                                  IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3),
                                  // Lanczos downscales of 2 .. 3 : 1 (windows 2 or 3 rows apart; 2 columns per thread)
@@ -5082,7 +5082,10 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  {true, 12, 7, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 12, 7, 4, 2, 3>)},
                                  {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, 4, 2, 3>)},
                                  {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, 4, 2, 3>)},
-                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 3>)}};
+                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 3>)},
+                                 // Area downscales of 2 .. 3 : 1
+                                 {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, 4, 2, 3>)},
+                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, 4, 2, 3>)}};
 #undef IQO_RYG_N
 #undef IQO_RYG
     const void *kern = nullptr;

@@ -1550,8 +1550,6 @@ void build_ryg(const Plan &p, RyxTables *t)
         return;
     const bool up = p.dstH > p.srcH;
     const int maxAdv = up ? 1 : p.srcH > 2 * p.dstH ? 3 : 2;  // window advance per output row (rows loaded)
-    if (maxAdv == 3 && p.method != kLanczos)
-        return;
     if (up && p.method != kLanczos)
         return;
     const int T = p.y.taps;
@@ -1585,12 +1583,16 @@ void build_ryg(const Plan &p, RyxTables *t)
     // 0.199 vs 0.271 ms, profiles/r05/steady_ryg_area.txt)
     static const Shape kShapes[] = {{kLanczos, 4, 3},  {kLanczos, 6, 4},  {kLanczos, 8, 5},  {kLanczos, 10, 5},
                                     {kLanczos, 10, 6}, {kLanczos, 12, 7}, {kArea, 3, 2},     {kArea, 3, 3},
-                                    {kLanczos, 14, 8}, {kLanczos, 16, 9}, {kLanczos, 18, 10}};
+                                    {kLanczos, 14, 8}, {kLanczos, 16, 9}, {kLanczos, 18, 10}, {kArea, 4, 3},
+                                    {kArea, 4, 4}};
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP && (!up || S.T <= 6) &&
-            (maxAdv == 3 ? S.T >= 10 && S.NP == S.T / 2 + 1 : S.T <= 12) &&  // (kernels.hip: NL = 3 shapes (T, T/2 + 1), T 10 .. 18)
+        if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP && (!up || S.T <= 8) &&
+            // (kernels.hip instantiations: NL = 3 Lanczos (T, T/2 + 1) for T 10 .. 18 and Area (4, 3 / 4);
+            // NL = 2 up to 12 taps; NL = 1 Lanczos 4, 6, 8 taps)
+            (maxAdv == 3 ? (p.method == kArea ? S.T == 4 : S.T >= 10 && S.NP == S.T / 2 + 1)
+                         : S.T <= 12 && !(p.method == kArea && S.T == 4)) &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;
     if (!best)

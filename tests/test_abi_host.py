@@ -103,7 +103,8 @@ def test_host_tables_match_oracle_random():
     (("lanczos", 3, 1920, 1080, 3840, 2160, 1), "lanczos_up2"),   # exact 2x Lanczos: register-window streamer
     (("lanczos", 3, 1921, 1080, 3842, 2160, 1), "ryg"),           # 2x rows on an odd width (round 5: ryg reads
                                                                   # rows that are not dword-aligned)
-    (("lanczos", 4, 1921, 1080, 3000, 2500, 1), "walk"),          # Lanczos-4 upscale (no ryg shape): wave walker
+    (("lanczos", 4, 1921, 1080, 3000, 2500, 1), "ryg"),           # Lanczos-4 upscale rows (round 5)
+    (("lanczos", 5, 1000, 700, 1500, 1000, 1), "walk"),           # Lanczos-5 upscale (no ryg shape): wave walker
     (("lanczos", 2, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-2
     (("lanczos", 4, 1920, 1080, 1280, 720, 1), "ryg"),             # 3:2 Lanczos-4: general rows (1 or 2 apart)
     (("lanczos", 3, 1920, 1080, 1366, 768, 1), "ryg"),             # rows 45:32
