@@ -1040,7 +1040,7 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     if (t.general) {
         d.cpt = h->rygCpt ? h->rygCpt
                           : std::min(t.taps >= 12 || t.NP >= 6 ? 3 : 4, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
-        if (t.rowLoads == 3)
+        if (t.rowLoads >= 3)
             d.cpt = 2;  // (downscales past 2:1: 2 columns per thread is the only instantiation)
         // (12-row windows or 6 column pairs with 4 columns per thread spill: 3 at most there)
         const int tw = h->ryxSplit == 2 ? 128 : 64;

@@ -3804,10 +3804,10 @@ struct RygArgs {
 };
 
 template <bool LZ, int T, int NP, int PD, int CPT, int NL>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryg_kernel(RygArgs a)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 18 ? 2 : 4))) void ryg_kernel(RygArgs a)
 {
     static_assert(CPT >= 2 && CPT <= 4, "output columns per thread");
-    static_assert(NL >= 1 && NL <= 3, "rows loaded per output row: 1 (upscales), 2 (down to 2:1), 3 (down to 3:1)");
+    static_assert(NL >= 1 && NL <= 4, "rows loaded per output row: 1 (upscales), 2 .. 4 (down to 2:1 .. 4:1)");
     constexpr int NPK = (CPT + 1) / 2;  // packed column pairs (an odd CPT: the last pair repeats its column)
     constexpr int OOB = 0x7ff00000;
     constexpr int PADB = 2 * kRyxPadK;  // work-row byte padding left of column 0
@@ -5085,7 +5085,16 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 3>)},
                                  // Area downscales of 2 .. 3 : 1
                                  {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, 4, 2, 3>)},
-                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, 4, 2, 3>)}};
+                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, 4, 2, 3>)},
+                                 // downscales of 3 .. 4 : 1 (windows 3 or 4 rows apart)
+                                 {true, 14, 8, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, 4, 2, 4>)},
+                                 {true, 16, 9, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, 4, 2, 4>)},
+                                 {true, 18, 10, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 4>)},
+                                 {true, 20, 11, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 20, 11, 4, 2, 4>)},
+                                 {true, 22, 12, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 12, 4, 2, 4>)},
+                                 {true, 24, 13, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 24, 13, 4, 2, 4>)},
+                                 {false, 5, 3, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 3, 4, 2, 4>)},
+                                 {false, 5, 4, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 4, 4, 2, 4>)}};
 #undef IQO_RYG_N
 #undef IQO_RYG
     const void *kern = nullptr;

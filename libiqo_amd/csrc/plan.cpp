@@ -1546,10 +1546,11 @@ void build_ryg(const Plan &p, RyxTables *t)
     // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart), or
     // grow (round 5: windows 0 or 1 rows apart, one new row per output row); widths as ryx_kernel
     if ((p.method != kLanczos && p.method != kArea) || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 ||
-        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 3 * p.dstH)
+        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 4 * p.dstH)
         return;
     const bool up = p.dstH > p.srcH;
-    const int maxAdv = up ? 1 : p.srcH > 2 * p.dstH ? 3 : 2;  // window advance per output row (rows loaded)
+    // window advance per output row (= rows loaded per output row)
+    const int maxAdv = up ? 1 : p.srcH > 3 * p.dstH ? 4 : p.srcH > 2 * p.dstH ? 3 : 2;
     if (up && p.method != kLanczos)
         return;
     const int T = p.y.taps;
@@ -1584,15 +1585,17 @@ void build_ryg(const Plan &p, RyxTables *t)
     static const Shape kShapes[] = {{kLanczos, 4, 3},  {kLanczos, 6, 4},  {kLanczos, 8, 5},  {kLanczos, 10, 5},
                                     {kLanczos, 10, 6}, {kLanczos, 12, 7}, {kArea, 3, 2},     {kArea, 3, 3},
                                     {kLanczos, 14, 8}, {kLanczos, 16, 9}, {kLanczos, 18, 10}, {kArea, 4, 3},
-                                    {kArea, 4, 4}};
+                                    {kArea, 4, 4},     {kLanczos, 20, 11}, {kLanczos, 22, 12}, {kLanczos, 24, 13},
+                                    {kArea, 5, 3},     {kArea, 5, 4}};
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
         if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP && (!up || S.T <= 8) &&
             // (kernels.hip instantiations: NL = 3 Lanczos (T, T/2 + 1) for T 10 .. 18 and Area (4, 3 / 4);
             // NL = 2 up to 12 taps; NL = 1 Lanczos 4, 6, 8 taps)
-            (maxAdv == 3 ? (p.method == kArea ? S.T == 4 : S.T >= 10 && S.NP == S.T / 2 + 1)
-                         : S.T <= 12 && !(p.method == kArea && S.T == 4)) &&
+            (maxAdv == 4   ? (p.method == kArea ? S.T == 5 : S.T >= 14 && S.NP == S.T / 2 + 1)
+             : maxAdv == 3 ? (p.method == kArea ? S.T == 4 : S.T >= 10 && S.T <= 18 && S.NP == S.T / 2 + 1)
+                           : S.T <= 12 && !(p.method == kArea && S.T >= 4)) &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;
     if (!best)
