@@ -82,6 +82,7 @@ CONFIGS = {
     "w4": ("lanczos", 3, 3840, 2160, 1366, 768, 1, 128, "W4 Lanczos-3 U8 1ch 3840x2160->1366x768"),
     "w5": ("area", 0, 3840, 2160, 1366, 768, 1, 128, "W5 Area U8 1ch 3840x2160->1366x768"),
     "w6": ("lanczos", 3, 3840, 2160, 1024, 576, 1, 128, "W6 Lanczos-3 U8 1ch 3840x2160->1024x576"),
+    "w7": ("linear", 0, 1920, 1080, 1366, 768, 1, 256, "W7 Linear U8 1ch 1920x1080->1366x768"),
 }
 
 

@@ -3456,7 +3456,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !
 #endif
     const int span = cHi - cLo;  // this workgroup's source columns [cLo, cHi), 4 per thread
     // a source width that is not a multiple of 4 (round 5): the thread straddling the row end loads
-    // the dword ending at the last column and shifts it down, so it never reads past the row and its
+    // the dword ending at the last column and the byte selectors shift it down, so it never reads past the row and its
     // columns past the end are zero (the masked border taps)
     const int vsh = 4 * t < span ? max(0, cLo + 4 * t + 4 - d.srcW) : 0;
     const int voff = 4 * t < span && IQO_RYX_EXP != 1 ? cLo + 4 * t - vsh : OOB;
@@ -3563,11 +3563,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !
     const int rowOff0 = (rBase - srcRow0) * srcSt;
     auto load_row = [&](int q) -> uint32_t {
         const bool in = static_cast<unsigned>(q - qLo) <= static_cast<unsigned>(qHi - qLo);
-        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? rowOff0 + q * srcSt : OOB), 0, 0) >> (8 * vsh);
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (in ? rowOff0 + q * srcSt : OOB), 0, 0);
     };
+    // (the straddling thread's shift is folded into the byte selectors: a selector byte 4 .. 6 picks
+    // a byte of the zero operand, so columns past the row end widen to zero with no extra VALU)
+    const uint32_t selLo = 0x0c010c00u + 0x00010001u * static_cast<uint32_t>(vsh);
+    const uint32_t selHi = 0x0c030c02u + 0x00010001u * static_cast<uint32_t>(vsh);
     auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
-        W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
-        W[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
+        W[0] = __builtin_amdgcn_perm(0u, v, selLo);
+        W[1] = __builtin_amdgcn_perm(0u, v, selHi);
     };
 
     uint32_t R[NW][2];
@@ -3879,11 +3883,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 18 ? 2 
     // offset, one below it an offset past srcBytes, both outside the buffer range (no compares;
     // prep_ryg checks that the offsets stay within 31 bits)
     auto load_row = [&](int r) -> uint32_t {
-        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (r - srcRow0) * srcSt, 0, 0) >> (8 * vsh);
+        return __builtin_amdgcn_raw_buffer_load_b32(srcR, voff + (r - srcRow0) * srcSt, 0, 0);
     };
+    // (the straddling thread's shift is in the byte selectors, as ryx_kernel)
+    const uint32_t selLo = 0x0c010c00u + 0x00010001u * static_cast<uint32_t>(vsh);
+    const uint32_t selHi = 0x0c030c02u + 0x00010001u * static_cast<uint32_t>(vsh);
     auto widen = [&](uint32_t v, uint32_t (&W)[2]) {
-        W[0] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
-        W[1] = __builtin_amdgcn_perm(0u, v, 0x0c030c02u);
+        W[0] = __builtin_amdgcn_perm(0u, v, selLo);
+        W[1] = __builtin_amdgcn_perm(0u, v, selHi);
     };
     // (plan.cpp build_ryg repeats the last record kRygRecPad >= PD + 2 times: no clamp)
     auto rec_s = [&](int y) { return sld(d.rowRec, 4 * y); };

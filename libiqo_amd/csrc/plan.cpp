@@ -1545,10 +1545,19 @@ void build_ryg(const Plan &p, RyxTables *t)
     *t = RyxTables();
     // rows shrink by more than 1 and at most 2 (consecutive windows start 1 or 2 rows apart), or
     // grow (round 5: windows 0 or 1 rows apart, one new row per output row); widths as ryx_kernel
-    if ((p.method != kLanczos && p.method != kArea) || p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 ||
-        p.srcW < 16 || p.dstH < 4 || p.srcH == p.dstH || p.srcH > 4 * p.dstH)
+    if (p.x.identity || p.y.identity || p.srcW > 8192 || p.dstW > 4096 || p.srcW < 16 || p.dstH < 4 ||
+        p.srcH == p.dstH || p.srcH > 4 * p.dstH)
         return;
     const bool up = p.dstH > p.srcH;
+    // Linear (round 5): downscales by at most 2 on both axes (no clamped reads,
+    // IQOLinearResizerImpl_Generic.cpp:210-282, 327-407).  Its sums are Area's (16-bit vertical
+    // sums, the same x rounding), so it runs the Area instantiations with a zero third row tap; the
+    // replicated border row / column (one per side) is a one-tap window of weight 256 / 2^15, whose
+    // sum rounds as the reference's (v * 256 + 128) >> 8 does
+    const bool linear = p.method == kLinear;
+    if (linear && (up || p.srcH > 2 * p.dstH || p.srcW <= p.dstW || p.srcW > 2 * p.dstW))
+        return;
+    const int sm = linear ? static_cast<int>(kArea) : static_cast<int>(p.method);  // the kernel's arithmetic
     // window advance per output row (= rows loaded per output row)
     const int maxAdv = up ? 1 : p.srcH > 3 * p.dstH ? 4 : p.srcH > 2 * p.dstH ? 3 : 2;
     if (up && p.method != kLanczos)
@@ -1590,20 +1599,26 @@ void build_ryg(const Plan &p, RyxTables *t)
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
-        if (S.method == p.method && S.T >= TE && S.T <= T && needNP <= S.NP && (!up || S.T <= 8) &&
+        if (S.method == sm && S.T >= TE && S.T <= T + (linear ? 1 : 0) && needNP <= S.NP && (!up || S.T <= 8) &&
             // (kernels.hip instantiations: NL = 3 Lanczos (T, T/2 + 1) for T 10 .. 18 and Area (4, 3 / 4);
             // NL = 2 up to 12 taps; NL = 1 Lanczos 4, 6, 8 taps)
-            (maxAdv == 4   ? (p.method == kArea ? S.T == 5 : S.T >= 14 && S.NP == S.T / 2 + 1)
-             : maxAdv == 3 ? (p.method == kArea ? S.T == 4 : S.T >= 10 && S.T <= 18 && S.NP == S.T / 2 + 1)
-                           : S.T <= 12 && !(p.method == kArea && S.T >= 4)) &&
+            (maxAdv == 4   ? (sm == kArea ? S.T == 5 : S.T >= 14 && S.NP == S.T / 2 + 1)
+             : maxAdv == 3 ? (sm == kArea ? S.T == 4 : S.T >= 10 && S.T <= 18 && S.NP == S.T / 2 + 1)
+                           : S.T <= 12 && !(sm == kArea && S.T >= 4)) &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;
     if (!best)
         return;
     const int TK = best->T, NP = best->NP;
-    const int off = std::min(lo, T - TK);  // kernel window: taps [off, off + TK) of the reference's
+    const int off = TK > T ? 0 : std::min(lo, T - TK);  // kernel window: taps [off, off + TK) of the reference's
     // per-phase taps as (c, c) splats
-    t->rowCoef.assign(static_cast<size_t>(p.y.phases) * TK, 0u);
+    // (Linear: two more phases, the replicated first row (window from row 0) and last row (window
+    // from row srcH - 2, its second tap))
+    t->rowCoef.assign(static_cast<size_t>(p.y.phases + (linear ? 2 : 0)) * TK, 0u);
+    if (linear) {
+        t->rowCoef[static_cast<size_t>(p.y.phases) * TK] = 256u * 0x10001u;
+        t->rowCoef[static_cast<size_t>(p.y.phases + 1) * TK + 1] = 256u * 0x10001u;
+    }
     for (int j = 0; j < p.y.phases; ++j)
         for (int k = 0; k < T; ++k) {
             const int32_t c = p.y.table[static_cast<size_t>(j * T + k)];
@@ -1626,14 +1641,17 @@ void build_ryg(const Plan &p, RyxTables *t)
         const CoordInfo &ci = p.y.coord[static_cast<size_t>(y)];
         if (ci.kind == kIdentity || ci.tabOff % T)
             return;
-        const int s0 = ci.srcO + off;
+        const bool lb = linear && ci.kind != kMain;  // Linear replicated border row
+        if (lb && (ci.kind != kBorderLo && ci.kind != kBorderHi))
+            return;
+        const int s0 = lb ? (ci.kind == kBorderLo ? 0 : p.srcH - 2) : ci.srcO + off;
         if (y > 0) {
             const int adv = s0 - t->rowRec[static_cast<size_t>(2 * y - 2)];
             if (adv < (up ? 0 : maxAdv - 1) || adv > maxAdv)
                 return;
         }
         t->rowRec[static_cast<size_t>(2 * y)] = s0;
-        t->rowRec[static_cast<size_t>(2 * y + 1)] = ci.tabOff / T * TK;
+        t->rowRec[static_cast<size_t>(2 * y + 1)] = lb ? (p.y.phases + (ci.kind == kBorderLo ? 0 : 1)) * TK : ci.tabOff / T * TK;
         if (p.method == kLanczos) {
             const Window win = axis_window(p, p.y, y, false);
             if (!win.border) {
@@ -1703,13 +1721,27 @@ static void column_nonzero(const Plan &p, int x, int *first, int *last)
     *last = b;
 }
 
+// Linear's replicated border column: a one-tap window on the first / last source column
+static bool linear_border_column(const Plan &p, int x, int *start)
+{
+    const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
+    if (p.method != kLinear || ci.kind == kMain || ci.kind == kIdentity)
+        return false;
+    *start = ci.kind == kBorderLo ? 0 : p.srcW - 1;
+    return true;
+}
+
 int ryx_column_pairs(const Plan &p)
 {
     int need = 0;
     for (int x = 0; x < p.dstW; ++x) {
-        int a, b;
+        int a, b, lbs;
         column_nonzero(p, x, &a, &b);
-        const int start = p.x.coord[static_cast<size_t>(x)].srcO + a;
+        if (linear_border_column(p, x, &lbs)) {
+            a = 0;
+            b = 0;
+        }
+        const int start = linear_border_column(p, x, &lbs) ? lbs : p.x.coord[static_cast<size_t>(x)].srcO + a;
         need = std::max(need, (start + (b - a) - (start & ~1)) / 2 + 1);
     }
     return need;
@@ -1726,15 +1758,18 @@ bool ryx_columns(const Plan &p, int NP, RyxTables *t)
         const CoordInfo &ci = p.x.coord[static_cast<size_t>(x)];
         if (ci.kind == kIdentity)
             return false;
-        int k0, k1;
+        int k0, k1, lbs;
         column_nonzero(p, x, &k0, &k1);
-        const int start = ci.srcO + k0;
+        const bool lb = linear_border_column(p, x, &lbs);
+        if (lb)
+            k1 = k0;
+        const int start = lb ? lbs : ci.srcO + k0;
         const int a = start & ~1;  // even start (floor)
         if (a < -kRyxPad || a + 2 * NP > p.srcW + kRyxPad || start - a + (k1 - k0) >= 2 * NP)
             return false;
         std::vector<int32_t> c(static_cast<size_t>(2 * NP), 0);
         for (int k = k0; k <= k1; ++k)
-            c[static_cast<size_t>(start - a + k - k0)] = p.x.table[static_cast<size_t>(ci.tabOff + k)];
+            c[static_cast<size_t>(start - a + k - k0)] = lb ? 1 << 15 : p.x.table[static_cast<size_t>(ci.tabOff + k)];
         for (int q = 0; q < NP; ++q)
             t->colCoef[static_cast<size_t>(x) * NP + q] = (static_cast<uint32_t>(c[static_cast<size_t>(2 * q)]) & 0xffffu) |
                                                        (static_cast<uint32_t>(c[static_cast<size_t>(2 * q + 1)]) << 16);

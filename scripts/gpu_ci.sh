@@ -26,7 +26,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 ARGS="$*"
 [ -z "$ARGS" ] && ARGS="tests bench"
-ALLCFGS="c1 c2 c3 c4 g1 g2 g3 g4 g5 g6 n1 n2 h1 h2 h3 h4 h5 h6 h7 h8 h9 w1 w2 w3 w4 w5 w6 u1 u2 u3"
+ALLCFGS="c1 c2 c3 c4 g1 g2 g3 g4 g5 g6 n1 n2 h1 h2 h3 h4 h5 h6 h7 h8 h9 w1 w2 w3 w4 w5 w6 w7 u1 u2 u3"
 for target in $ARGS; do
 case $target in
 tests)

@@ -118,7 +118,9 @@ def test_host_tables_match_oracle_random():
     (("area", 0, 1920, 1080, 1280, 720, 1), "area_d32"),          # exact 3:2 Area: no window, no halo
     (("lanczos", 3, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-3: register window
     (("area", 0, 1921, 1080, 1280, 720, 1), "ryg"),              # (odd width: ryg since round 5)
-    (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),
+    (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),             # Linear upscale rows: walker
+    (("linear", 0, 1920, 1080, 1366, 768, 1), "ryg"),              # Linear downscale to 2:1 (round 5)
+    (("linear", 0, 1920, 1080, 900, 500, 1), "tile"),              # beyond 2:1 (the reference reads past the row)
     (("lanczos", 3, 13, 9, 5, 40, 1), "tile"),                    # 13 columns: no 256-column strip fits the walker's tables
     (("lanczos", 9, 64, 48, 1000, 900, 1), "tile"),               # 64 work columns per row window: tiles
     (("lanczos", 3, 1920, 1080, 960, 540, 2), "lanczos_stream"),   # pxScale-2 chroma (ring streamer)
