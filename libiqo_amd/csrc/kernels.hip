@@ -3807,8 +3807,11 @@ struct RygArgs {
     unsigned nBlocks;
 };
 
+// (occupancy: two 512-thread workgroups per CU up to 22 row taps -- at 22 the compiler spills a few
+// registers and the kernel is still 5.5 % faster than at one workgroup per CU, 4K -> 1024x576
+// profiles/r05/steady_ryg_wpe.txt; 24 taps stay at one)
 template <bool LZ, int T, int NP, int PD, int CPT, int NL>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 18 ? 2 : 4))) void ryg_kernel(RygArgs a)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 22 ? 2 : 4))) void ryg_kernel(RygArgs a)
 {
     static_assert(CPT >= 2 && CPT <= 4, "output columns per thread");
     static_assert(NL >= 1 && NL <= 4, "rows loaded per output row: 1 (upscales), 2 .. 4 (down to 2:1 .. 4:1)");
