@@ -11,7 +11,7 @@ tail -1 $OUT/bench_driver.log > $OUT/bench_driver.json
 cd /tmp || exit 1
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_drv" -o run -- python3 "$ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu --no-probe > "$OUT/prof_drv.log" 2>&1 || { echo "prof failed"; tail -5 "$OUT/prof_drv.log"; exit 1; }
-tail -1 "$OUT/prof_drv.log" > "$OUT/bench_line_under_rocprof.json"
+grep '^{"metric"' "$OUT/prof_drv.log" > "$OUT/bench_line_under_rocprof.json"
 cd "$ROOT" || exit 1
 PMC_CFGS="c2" bash scripts/gpu_ci.sh pmc || exit 1
 python3 scripts/pmc_to_json.py gpurun_out c2 --round r05
