@@ -59,6 +59,13 @@ SHAPES = [
     ("area", 0, 1920, 1080, 1366, 768),
     ("lanczos", 2, 1920, 1080, 1024, 576),
     ("linear", 0, 1920, 1080, 1280, 720),
+    # round 5, late: ryg past 2:1, Linear on ryg, upscale rows
+    ("lanczos", 3, 3840, 2160, 1366, 768),
+    ("area", 0, 3840, 2160, 1366, 768),
+    ("lanczos", 3, 3840, 2160, 1024, 576),
+    ("linear", 0, 1920, 1080, 1366, 768),
+    ("lanczos", 3, 1366, 768, 1920, 1080),
+    ("lanczos", 3, 1024, 576, 1920, 1080),
 ]
 
 
