@@ -1207,6 +1207,16 @@ bool ryg_usable(const iqo_hip_plan *h)
     return h->ryx.ok && h->ryx.general && h->useRyg && ryx_dev(h).parts > 0;
 }
 
+// Area and Linear rows shrinking by less than 1.4, or with two row phases (exact 3:2), keep the wave
+// walker when it can run: ryg loads NL = 2 rows per output row and is slower there (steady clock,
+// x256: Area 1080p -> 1600x900 0.368 vs 0.267 ms, 1440p -> 1080p 0.415 vs 0.356, Linear 3:2 0.181
+// vs 0.163; at 45:32 ryg is ahead, Area 0.198 vs 0.271; profiles/r05/ratio_sweep_ryg_ab.txt)
+bool walk_beats_ryg(const iqo_hip_plan *h)
+{
+    const Plan &p = h->p;
+    return p.method != iqo_amd::kLanczos && (5 * p.srcH < 7 * p.dstH || p.y.phases <= 2);
+}
+
 // The kernel family a full-frame call with aligned pointers and strides runs.
 int plan_kernel(const iqo_hip_plan *h)
 {
@@ -1232,7 +1242,7 @@ int plan_kernel(const iqo_hip_plan *h)
     if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && h->lt.ok && h->useL23)
         k = IQO_KERNEL_LINEAR_U23;
     // general rows last: only what no exact-ratio kernel takes
-    if ((k == IQO_KERNEL_WALK || k == IQO_KERNEL_TILE) && ryg_usable(h))
+    if ((k == IQO_KERNEL_TILE || (k == IQO_KERNEL_WALK && !walk_beats_ryg(h))) && ryg_usable(h))
         k = IQO_KERNEL_RYG;
     return k;
 }
@@ -1288,8 +1298,7 @@ int kernel_for_layout(const iqo_hip_plan *h, const void *src, size_t srcSt, size
         aligned(src, 8, srcSt, srcFrameSt) && aligned(dst, 4, dstSt, dstFrameSt))
         kernel = IQO_KERNEL_LINEAR_U23;
     // general rows last (dword loads, byte stores)
-    if ((kernel == IQO_KERNEL_WALK || kernel == IQO_KERNEL_TILE) &&
-        ryg_usable(h))
+    if ((kernel == IQO_KERNEL_TILE || (kernel == IQO_KERNEL_WALK && !walk_beats_ryg(h))) && ryg_usable(h))
         kernel = IQO_KERNEL_RYG;
     return kernel;
 }

@@ -66,6 +66,15 @@ SHAPES = [
     ("linear", 0, 1920, 1080, 1366, 768),
     ("lanczos", 3, 1366, 768, 1920, 1080),
     ("lanczos", 3, 1024, 576, 1920, 1080),
+    ("linear", 0, 1920, 1080, 1024, 576),
+    ("linear", 0, 1920, 1080, 1600, 900),
+    ("linear", 0, 2560, 1440, 1920, 1080),
+    ("linear", 0, 3840, 2160, 2560, 1440),
+    ("lanczos", 3, 2560, 1440, 1920, 1080),
+    ("lanczos", 3, 1920, 1080, 1600, 900),
+    ("lanczos", 2, 1920, 1080, 1600, 900),
+    ("area", 0, 2560, 1440, 1920, 1080),
+    ("area", 0, 1920, 1080, 1600, 900),
 ]
 
 

@@ -117,7 +117,10 @@ def test_host_tables_match_oracle_random():
     (("linear", 0, 1280, 720, 1920, 1080, 1), "linear_u23"),      # exact 2:3 Linear upscale
     (("area", 0, 1920, 1080, 1280, 720, 1), "area_d32"),          # exact 3:2 Area: no window, no halo
     (("lanczos", 3, 1920, 1080, 1280, 720, 1), "lanczos_d32"),    # exact 3:2 Lanczos-3: register window
-    (("area", 0, 1921, 1080, 1280, 720, 1), "ryg"),              # (odd width: ryg since round 5)
+    (("area", 0, 1921, 1080, 1280, 720, 1), "walk"),             # (odd width: the walker when the rows are
+                                                                  # 4-byte aligned, else ryg)
+    (("area", 0, 1920, 1080, 1600, 900, 1), "walk"),             # Area / Linear rows shrinking by < 1.4: walker
+    (("linear", 0, 1920, 1080, 1280, 720, 1), "walk"),           # Linear 3:2 (two row phases): walker
     (("linear", 0, 1366, 768, 1000, 1000, 1), "walk"),             # Linear upscale rows: walker
     (("linear", 0, 1920, 1080, 1366, 768, 1), "ryg"),              # Linear downscale to 2:1 (round 5)
     (("linear", 0, 1920, 1080, 900, 500, 1), "tile"),              # beyond 2:1 (the reference reads past the row)
