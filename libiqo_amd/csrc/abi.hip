@@ -1038,15 +1038,27 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // 0.308 (a third of the threads idle in the horizontal pass), 2 columns needed four parts
     // (profiles/r05/steady_ryg_cpt.txt); option "ryg_cpt" forces 2, 3 or 4
     if (t.general) {
-        d.cpt = h->rygCpt ? h->rygCpt
-                          : std::min(t.taps >= 12 || t.NP >= 6 ? 3 : 4, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
+        const int cap = t.taps >= 12 || t.NP >= 6 ? 3 : 4;  // (12-row windows or 6 column pairs with 4
+                                                            // columns per thread spill: 3 at most there)
+        d.cpt = h->rygCpt ? h->rygCpt : std::min(cap, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
         if (t.rowLoads >= 3)
             d.cpt = 2;  // (downscales past 2:1: 2 columns per thread is the only instantiation)
-        // (12-row windows or 6 column pairs with 4 columns per thread spill: 3 at most there)
         const int tw = h->ryxSplit == 2 ? 128 : 64;
-        if ((h->ryxSplit >= 2 && split_min(tw)) || (h->ryxSplit == 1 && split(2, 256)) || split(1, 512) ||
-            split_min(512))  // (ryx_split 0: one 8-wave part where it fits)
-            return d;
+        if ((h->ryxSplit >= 2 && split_min(tw)) || (h->ryxSplit == 1 && split(2, 256)) || split(1, 512))
+            return d;  // (ryx_split 0: one 8-wave part where it fits)
+        // (round 5, late) one more column per thread when that keeps the row in one workgroup, else
+        // the fewest parts, each of the fewest 64-thread multiples that hold it: 1080p -> 1600x900
+        // had two 512-thread parts with half their threads idle
+        if (!h->rygCpt && t.rowLoads < 3 && d.cpt < cap) {
+            ++d.cpt;
+            if (split(1, 512))
+                return d;
+            --d.cpt;
+        }
+        for (int n = 2; n <= 16; ++n)
+            for (int th = 128; th <= 512; th += 64)
+                if (split(n, th))
+                    return d;
         d.cpt = 2;
         d.parts = 0;
     }
