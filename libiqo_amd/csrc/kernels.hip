@@ -5077,9 +5077,9 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
         const void *kern;
     };
 #define IQO_RYG_N(LZ_, T_, NP_, NL_)                                                                   \
-    {LZ_, T_, NP_, 2, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 2, NL_>)},    \
-    {LZ_, T_, NP_, 3, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 3, NL_>)},    \
-    {LZ_, T_, NP_, 4, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, 4, 4, NL_>)}
+    {LZ_, T_, NP_, 2, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 2, NL_>)},    \
+    {LZ_, T_, NP_, 3, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 3, NL_>)},    \
+    {LZ_, T_, NP_, 4, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 4, NL_>)}
 #define IQO_RYG(LZ_, T_, NP_) IQO_RYG_N(LZ_, T_, NP_, 2)
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
@@ -5088,23 +5088,23 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)
                                  IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3),
                                  // Lanczos downscales of 2 .. 3 : 1 (windows 2 or 3 rows apart; 2 columns per thread)
-                                 {true, 10, 6, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 10, 6, 4, 2, 3>)},
-                                 {true, 12, 7, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 12, 7, 4, 2, 3>)},
-                                 {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, 4, 2, 3>)},
-                                 {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, 4, 2, 3>)},
-                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 3>)},
+                                 {true, 10, 6, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 10, 6, kRygPD, 2, 3>)},
+                                 {true, 12, 7, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 12, 7, kRygPD, 2, 3>)},
+                                 {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 3>)},
+                                 {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 3>)},
+                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 3>)},
                                  // Area downscales of 2 .. 3 : 1
-                                 {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, 4, 2, 3>)},
-                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, 4, 2, 3>)},
+                                 {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, kRygPD, 2, 3>)},
+                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, kRygPD, 2, 3>)},
                                  // downscales of 3 .. 4 : 1 (windows 3 or 4 rows apart)
-                                 {true, 14, 8, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, 4, 2, 4>)},
-                                 {true, 16, 9, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, 4, 2, 4>)},
-                                 {true, 18, 10, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, 4, 2, 4>)},
-                                 {true, 20, 11, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 20, 11, 4, 2, 4>)},
-                                 {true, 22, 12, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 12, 4, 2, 4>)},
-                                 {true, 24, 13, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 24, 13, 4, 2, 4>)},
-                                 {false, 5, 3, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 3, 4, 2, 4>)},
-                                 {false, 5, 4, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 4, 4, 2, 4>)}};
+                                 {true, 14, 8, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 4>)},
+                                 {true, 16, 9, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 4>)},
+                                 {true, 18, 10, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 4>)},
+                                 {true, 20, 11, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 20, 11, kRygPD, 2, 4>)},
+                                 {true, 22, 12, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 12, kRygPD, 2, 4>)},
+                                 {true, 24, 13, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 24, 13, kRygPD, 2, 4>)},
+                                 {false, 5, 3, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 3, kRygPD, 2, 4>)},
+                                 {false, 5, 4, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 4, kRygPD, 2, 4>)}};
 #undef IQO_RYG_N
 #undef IQO_RYG
     const void *kern = nullptr;

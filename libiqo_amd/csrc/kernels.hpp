@@ -144,7 +144,10 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
 
 // General-row variant (plan.hpp build_ryg; kernels.hip ryg_kernel): ryx's tabled columns and column
 // parts, rows from a per-row record table instead of an exact P:Q.
-constexpr int kRygPD = 4;  // ryg_kernel: output rows loaded ahead (the instantiations' PD)
+#ifndef IQO_RYG_PD
+#define IQO_RYG_PD 4  // (variant builds: 6; plan.hpp kRygRecPad must stay >= PD + 2)
+#endif
+constexpr int kRygPD = IQO_RYG_PD;  // ryg_kernel: output rows loaded ahead (the instantiations' PD)
 struct RygDev {
     bool lanczos;
     int srcW, srcH, dstW, dstH;
