@@ -11,16 +11,22 @@ process per GPU, plus the HBM roofline fraction of the kernel.
 --shard image (default): each rank resizes its own device-resident batch of B frames (weak
   scaling, no data-path collective).  A "step" = one libiqo_hip launch over the rank's batch.
 --shard band: every frame of one global batch of B frames is split by output-row band over the
-  ranks (libiqo_amd/shard.py): each rank uploads its source window (halo rows) from host memory,
-  a step = one iqo_hip_resize_band launch over its band of all B frames, and the bands are
-  gathered to rank 0 by IPC handle + device copy.  Window upload and gather are timed once,
-  separately from the compute steps.
+  ranks (libiqo_amd/shard.py): each rank holds only its source window (the halo rows its band
+  reads) of every frame, generated on its device from per-frame seeds (frame f is reproducible
+  from f alone; --band-src host stages the window in pinned host memory instead and uploads it,
+  timed as `scatter_ms`), a step = one iqo_hip_resize_band launch over its band of all B frames,
+  and the bands are gathered to rank 0 by IPC handle + device copy, timed once, separately from
+  the compute steps.  No rank allocates the global source batch.
 
 Inputs are synthetic uniform-random U8 frames generated before timing.  Image mode cycles through
 several distinct device batches, one per step (--rotate; auto: >= 3 batches and >= 2.5 GB per cycle): relaunching
 the SAME batch lets the 256 MiB Infinity Cache serve part of the reads (C2: ~15 % faster), which no
 real pipeline sees; that figure is reported separately as reuse_probe.  Rank 0 prints ONE JSON
-line.  The CPU baseline (rank 0, N=1 only) times the reference's own CPU path -- its public
+line.  With the default config (C2) at N = 1 the line also carries `secondary`: C3 (64 frames) and
+C4 (256 frames) timed the same way on their own rotated batches, with parity on frames 0, mid and
+last, and a plain streaming kernel of each config's read:write byte mix (libiqo_probe.so) on the
+same buffers -- the on-box ceiling each kernel's fraction can be read against.
+The CPU baseline (rank 0, N=1 only) times the reference's own CPU path -- its public
 classes with their CPUID dispatch (AVX512 on the node) and OpenMP, compiled from its sources into
 oracle/_ref -- plus its Generic impl, on the host CPUs this process may use, over a bounded
 sample of the same workload.
@@ -293,6 +299,168 @@ def alt_batch(make_step, frames_alt, bytes_per_frame, dev, steps=20, settle_ms=6
             "achieved": round(gbps, 1), "frac": round(gbps / HBM_PEAK_GBPS, 4), "untimed_launches": n}
 
 
+BAND_SEED = 1234
+
+
+def band_frame(f, sh, sw, device):
+    """Source frame f of the band-mode batch: uniform random U8 from seed BAND_SEED + f, so any frame
+    can be regenerated from its index alone (rank 0 regenerates the checked frames for parity)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(BAND_SEED + f)
+    return torch.randint(0, 256, (sh, sw), dtype=torch.uint8, device=device, generator=g)
+
+
+def band_window(frames, s0, s1, sh, sw, device):
+    """Rows [s0, s1) of every band-mode frame, [frames, s1 - s0, sw] on `device`: one frame is
+    generated at a time and only its window rows are kept."""
+    import torch
+    win = torch.empty((frames, s1 - s0, sw), dtype=torch.uint8, device=device)
+    for f in range(frames):
+        win[f].copy_(band_frame(f, sh, sw, device)[s0:s1])
+    return win
+
+
+def band_buffers(resizer, frames, sw, dw, dh, rank, world, device, band_src="device", rot=0):
+    """This rank's band-mode buffers, bounded by its own shard (shard.band_plan), never by the global
+    batch: `rot` device copies of its source window [frames, s1 - s0, sw] and of its output band
+    [frames, r1 - r0, dw], plus -- band_src == "host" -- the window staged in (pinned) host memory
+    for the timed upload.  Returns (shard, host_window or None, [device windows], [device bands])."""
+    import torch
+
+    from libiqo_amd import shard as shard_mod
+    mine = shard_mod.make_shards(resizer, dh, list(range(world)))[rank]
+    srows, rows = mine.s1 - mine.s0, mine.r1 - mine.r0
+    bytes_launch = float(frames) * (srows * sw + rows * dw)
+    rot = rot or max(2, int(-(-2.5e9 // max(bytes_launch, 1.0))))
+    host = None
+    if band_src == "host":
+        host = band_window(frames, mine.s0, mine.s1, resizer.srcH, sw, device).cpu()
+        if torch.cuda.is_available():
+            host = host.pin_memory()
+        wins = []
+    else:
+        wins = [band_window(frames, mine.s0, mine.s1, resizer.srcH, sw, device)]
+    bands = [torch.empty((frames, rows, dw), dtype=torch.uint8, device=device) for _ in range(rot)]
+    return mine, host, wins, bands, rot
+
+
+def probe_lib():
+    """libiqo_amd/libiqo_probe.so: a streaming read:write kernel (measurement only)."""
+    import ctypes
+    L = ctypes.CDLL(os.path.join(ROOT, "libiqo_amd", "libiqo_probe.so"))
+    L.iqo_probe_stream.restype = ctypes.c_int
+    L.iqo_probe_stream.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    return L
+
+
+def settle_and_time(step, dev, stream, steps, settle_ms=150.0):
+    """~settle_ms of back-to-back untimed launches (the GPU's post-start clock dip is over, as
+    bench's auto warmup), then `steps` launches between two HIP events on the launch stream."""
+    import torch
+    t0 = time.perf_counter()
+    n = 0
+    while n < 3 or (time.perf_counter() - t0) * 1e3 < settle_ms:
+        step()
+        n += 1
+        if n % 8 == 0:
+            torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / steps, n
+
+
+# read:write byte mix of each config (source : output bytes per frame), as the probe's (R, W) units
+PROBE_MIX = {"c2": (4, 1), "c3": (16, 1), "c4": (1, 4)}
+
+
+def stream_probe(L, mix, src, src_bytes, dst, dst_bytes, dev, stream, steps):
+    """The streaming probe with the byte mix `mix` over the rotated buffers src[b] / dst[b] (the
+    kernel's own), plain and nontemporal stores; the faster is the ceiling."""
+    R, W = mix
+    units = min(src_bytes // (1024 * R), dst_bytes // (1024 * W))
+    moved = float(units) * 1024 * (R + W)
+    out = {"mix_read_write": "%d:%d" % (R, W), "bytes_per_launch": int(moved)}
+    sp = stream.cuda_stream
+    for nt in (0, 1):
+        k = [0]
+
+        def st():
+            b = k[0] % src.shape[0]
+            k[0] += 1
+            rc = L.iqo_probe_stream(R, W, nt, src[b].data_ptr(), src_bytes, dst[b].data_ptr(), dst_bytes, sp)
+            if rc:
+                raise RuntimeError("iqo_probe_stream failed (%d)" % rc)
+        ms, _ = settle_and_time(st, dev, stream, steps, settle_ms=60.0)
+        out["nt" if nt else "plain"] = {"ms_per_launch": round(ms, 4), "achieved": round(moved / (ms / 1e3) / 1e9, 1)}
+    best = max(out["plain"]["achieved"], out["nt"]["achieved"])
+    out["ceiling"] = best
+    out["ceiling_frac_of_peak"] = round(best / HBM_PEAK_GBPS, 4)
+    return out
+
+
+def secondary_config(name, frames, dev, stream, steps, verify, probe=None, make=None):
+    """One more BASELINE config timed like the headline (rotated fresh device batches, >= 3 and
+    >= 2.5 GB per cycle; time-based warmup; HIP events on the launch stream), its frames 0, mid and
+    last checked against the oracle, plus the streaming probe of its byte mix on the same buffers."""
+    import torch
+
+    import libiqo_amd
+    m, d, sw, sh, dw, dh, px, _, label = CONFIGS[name]
+    r = make(m, d, sw, sh, dw, dh, px) if make else libiqo_amd.make_resizer(m, d, sw, sh, dw, dh, px, device=dev.index)
+    kernel = r.describe()["kernel"]
+    bytes_launch = float(frames) * (sw * sh + dw * dh)
+    rot = max(3, int(-(-2.5e9 // bytes_launch)))
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5678)
+    src = torch.randint(0, 256, (rot, frames, sh, sw), dtype=torch.uint8, device=dev, generator=gen)
+    dst = torch.empty((rot, frames, dh, dw), dtype=torch.uint8, device=dev)
+    sp = stream.cuda_stream
+    k = [0]
+
+    def st():
+        b = k[0] % rot
+        k[0] += 1
+        r.resize_device(frames, sw, sw * sh, src[b].data_ptr(), dw, dw * dh, dst[b].data_ptr(), sp)
+    ms, n = settle_and_time(st, dev, stream, steps)
+    gbps = bytes_launch / (ms / 1e3) / 1e9
+    res = {"workload": label, "kernel": kernel, "frames": frames, "batches_cycled": rot, "steps": steps,
+           "untimed_launches": n, "kernel_ms_per_launch": round(ms, 4), "algorithmic_bytes_per_launch": int(bytes_launch),
+           "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "frac": round(gbps / HBM_PEAK_GBPS, 4),
+           "value_mpix_s": round(frames * dw * dh / (ms / 1e3) / 1e6, 1)}
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_%s.json" % name)) as f:
+            pmc = json.load(f)
+        if pmc.get("frames") == frames and pmc.get("kernel") == kernel:
+            res["traffic"] = pmc.get("hbm_bytes_per_launch")
+            res["traffic_source"] = "profiles/pmc_%s.json (round %s), not measured in this run" % (name, pmc.get("round"))
+    except Exception:
+        pass
+    if verify:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as ol
+        ok = True
+        for f in sorted({0, frames // 2, frames - 1}):
+            exp = ol.run_oracle(m, d, sw, sh, dw, dh, px, src[0, f].cpu().numpy())
+            ok = ok and bool((dst[0, f].cpu().numpy() == exp).all())
+        res["parity"] = "bit-exact vs Generic oracle (frames 0, mid, last)" if ok else "MISMATCH"
+    else:
+        res["parity"] = "unchecked"
+    if probe is not None:
+        res["stream_probe"] = stream_probe(probe, PROBE_MIX[name], src, frames * sw * sh, dst, frames * dw * dh, dev,
+                                           stream, steps)
+        res["frac_of_probe_ceiling"] = round(gbps / res["stream_probe"]["ceiling"], 4)
+    del src, dst
+    torch.cuda.empty_cache()
+    return res
+
+
 def spawn_ranks(n):
     """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the environment): start N
     rank processes of this same command line, one per GPU, as torch.distributed.run would (RANK /
@@ -340,6 +508,11 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (band mode: global frames; 0 = default)")
     ap.add_argument("--shard", default="image", choices=["image", "band"])
+    ap.add_argument("--band-src", default="device", choices=["device", "host"],
+                    help="band mode: each rank's source window generated on its device, or staged in pinned host "
+                         "memory and uploaded (timed as scatter_ms)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the C3 / C4 lines and the streaming probes the default C2 run carries at N = 1")
     ap.add_argument("--bands", type=int, default=0, help="row bands per frame inside a launch (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -356,6 +529,8 @@ def main():
     ap.add_argument("--spawn-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.option:
+        os.environ["IQO_HIP_TUNING"] = "1"  # the A/B option keys (include/iqo_hip.h iqo_hip_plan_set_option)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     if args.spawn_probe:
@@ -433,28 +608,30 @@ def main():
             nstep[0] += 1
     else:
         from libiqo_amd import shard
-        # the global source batch in pinned host memory, identical on every rank (same seed)
-        gen = torch.Generator()
-        gen.manual_seed(1234)
-        host_src = torch.randint(0, 256, (frames, sh, sw), dtype=torch.uint8, generator=gen).pin_memory()
+        # this rank's source window only (never the global batch): generated on its device from the
+        # per-frame seeds, or (--band-src host) staged in pinned host memory and uploaded, timed
         out = torch.zeros((frames, dh, dw), dtype=torch.uint8, device=dev) if rank == 0 else None
-        be = shard.HipBandBackend(lambda device: r if device == local else make(device), host_src, -1, out, local)
-        shards = shard.make_shards(r, dh, [local] * world if world == 1 else list(range(world)))
-        shards = [s._replace(device=local) if i == rank else s for i, s in enumerate(shards)]
-        mine = shards[rank]
-        t_sc = time.perf_counter()
-        win = be.scatter(mine)
-        torch.cuda.synchronize(dev)
-        t_sc = time.perf_counter() - t_sc
+        mine, host_win, wins, bands_out, rot = band_buffers(r, frames, sw, dw, dh, rank, world, dev, args.band_src,
+                                                            args.rotate)
+        mine = mine._replace(device=gpu)
+        t_sc = 0.0
+        be = shard.HipBandBackend(lambda device: r if device == mine.device else make(device),
+                                  host_win if host_win is not None else wins[0], -1 if host_win is not None else gpu,
+                                  out, gpu, src_row0=mine.s0)
+        if host_win is not None:
+            torch.cuda.synchronize(dev)
+            t_sc = time.perf_counter()
+            wins.append(be.scatter(mine))
+            torch.cuda.synchronize(dev)
+            t_sc = time.perf_counter() - t_sc
+        else:
+            be.paths["scatter"] = {"window generated on the rank's device (per-frame seeds): no upload"}
         rows, srows = mine.r1 - mine.r0, mine.s1 - mine.s0
-        band = torch.empty((frames, rows, dw), dtype=torch.uint8, device=dev)
         bytes_launch = float(frames) * (srows * sw + rows * dw)
         out_px_step = float(frames) * dw * dh  # the whole frame, all ranks together
         # like image mode, steps cycle through distinct copies of the window (>= 2.5 GB per cycle)
-        # so no step re-reads its input from the Infinity Cache; the uploaded window is copy 0
-        rot = args.rotate or max(2, int(-(-2.5e9 // bytes_launch)))
-        wins = [win] + [win.clone() for _ in range(rot - 1)]
-        bands_out = [band] + [torch.empty_like(band) for _ in range(rot - 1)]
+        # so no step re-reads its input from the Infinity Cache; copy 0 is the generated / uploaded one
+        wins += [wins[0].clone() for _ in range(rot - 1)]
         nstep = [0]
 
         def step():
@@ -525,7 +702,9 @@ def main():
         if dist:
             dist.barrier()
         t_g = time.perf_counter() - t_g
-        band_info = {"ranks": world, "rows_per_rank": rows, "src_window_rows": srows,
+        band_info = {"ranks": world, "rows_per_rank": rows, "src_window_rows": srows, "band_src": args.band_src,
+                     "rank_device_bytes": int(rot * frames * (srows * sw + rows * dw)),
+                     "rank_host_bytes": int(host_win.numel()) if host_win is not None else 0,
                      "scatter_ms": round(scatter_max * 1e3, 3), "gather_ms": round(t_g * 1e3, 3),
                      "scatter_path": sorted(be.paths.get("scatter", [])), "gather_path": sorted(be.paths.get("gather", []))}
 
@@ -537,8 +716,8 @@ def main():
         for f in sorted({0, frames // 2, frames - 1}):
             if args.shard == "image":
                 s_np, o_np = src[0, f].cpu().numpy(), dst[0, f].cpu().numpy()
-            else:
-                s_np, o_np = host_src[f].numpy(), out[f].cpu().numpy()
+            else:  # rank 0 regenerates the whole source frame from its seed
+                s_np, o_np = band_frame(f, sh, sw, dev).cpu().numpy(), out[f].cpu().numpy()
             exp = ol.run_oracle(m, d, sw, sh, dw, dh, px, s_np)
             ok = ok and bool((o_np == exp).all())
         parity = ("bit-exact vs Generic oracle (frames 0, mid, last%s)" %
@@ -583,6 +762,35 @@ def main():
         alt = alt_batch(make_alt, alt_frames, sw * sh + dw * dh, dev)
         log("alt batch: %s" % json.dumps(alt))
 
+    secondary = None
+    if rank == 0 and world == 1 and args.shard == "image" and args.config == "c2" and not args.no_secondary:
+        # C3 / C4 in the same run (the driver's record), after the headline and before the CPU leg
+        if "src" in locals():
+            del src, dst
+        torch.cuda.empty_cache()
+        secondary = {}
+        try:
+            pl = probe_lib()
+        except OSError as e:
+            pl = None
+            secondary["probe_error"] = str(e)
+        n_sec = max(20, min(args.steps, 50))
+        for name, nf in (("c3", 64), ("c4", 256)):
+            secondary[name] = secondary_config(name, nf, dev, stream, n_sec, not args.no_verify, pl, make=None)
+            log("secondary %s: %s" % (name, json.dumps(secondary[name])))
+            if secondary[name]["parity"] == "MISMATCH":
+                raise SystemExit("secondary %s MISMATCH" % name)
+        if pl is not None:
+            # the headline's own byte mix on fresh buffers of its size (C2 x frames)
+            g3 = torch.Generator(device=dev)
+            g3.manual_seed(91)
+            ps = torch.randint(0, 256, (3, frames * sh * sw), dtype=torch.uint8, device=dev, generator=g3)
+            pd = torch.empty((3, frames * dh * dw), dtype=torch.uint8, device=dev)
+            secondary["c2_stream_probe"] = stream_probe(pl, PROBE_MIX["c2"], ps, frames * sw * sh, pd, frames * dw * dh,
+                                                        dev, stream, n_sec)
+            del ps, pd
+            torch.cuda.empty_cache()
+
     cpu = None
     ref_bench = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -618,9 +826,10 @@ def main():
             "scaling": "weak" if args.shard == "image" else "strong",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: uniform random U8 frames (torch.randint, seed 1234%s)" %
-                    ("+rank, on device; %d distinct batches cycled, one per step" % rot if args.shard == "image"
-                     else ", pinned host, windows uploaded"),
+            "data": "synthetic: uniform random U8 frames (torch.randint, seed %s)" %
+                    ("1234+rank, on device; %d distinct batches cycled, one per step" % rot if args.shard == "image"
+                     else "%d + frame index; each rank generates only its source window (%s)" %
+                     (BAND_SEED, "on device" if args.band_src == "device" else "staged in pinned host memory, uploaded")),
             "config": {"workload": label, "frames_per_gpu": frames if args.shard == "image" else None,
                        "global_frames": frames * world if args.shard == "image" else frames,
                        "parallelism": par, "kernel": kernel, "bands_per_frame": args.bands or "auto",
@@ -646,6 +855,12 @@ def main():
             res["batch_alt"] = alt
         if probe:
             res["reuse_probe"] = probe
+        if secondary:
+            res["secondary"] = secondary
+            cp = secondary.get("c2_stream_probe")
+            if cp:
+                res["roofline"]["stream_probe_ceiling"] = cp["ceiling"]
+                res["roofline"]["frac_of_probe_ceiling"] = round(achieved / cp["ceiling"], 4)
         if ref_bench:
             res["reference_benchmark"] = ref_bench
         if cpu and cpu.get("value"):

@@ -104,20 +104,16 @@ int iqo_hip_plan_query(const iqo_hip_plan *plan, iqo_hip_plan_desc *desc);
  * arguments (the specialised fast kernels) have nothing to upload; the call is then a no-op. */
 int iqo_hip_plan_prepare(iqo_hip_plan *plan);
 
-/* Options (tests / tuning): "force_general" (0/1: every shape through IQO_KERNEL_GENERAL),
- * "bands" (row bands per frame, 0 = auto), "tile" (0: shapes without a specialised kernel use
- * IQO_KERNEL_GENERAL instead of IQO_KERNEL_TILE / _WALK), "walk" (0: IQO_KERNEL_TILE instead of
- * IQO_KERNEL_WALK / _LANCZOS_UP2; default 1), "up2" (0: IQO_KERNEL_WALK instead of
- * IQO_KERNEL_LANCZOS_UP2; default 1), "d32" / "a32" / "u23" / "l23" / "d31" / "ryx" / "ryg" (0: the
- * walker or tile kernel instead of IQO_KERNEL_LANCZOS_D32 / _AREA_D32 / _LANCZOS_U23 /
- * _LINEAR_U23 / _LANCZOS_D31 / _RYX / _RYG; default 1), "tile_rows" (output rows per tile, 0 = auto),
- * "stack" (0 / 1 / 2: narrow frames side by side in one workgroup off / where a frame fills at
- * most half a wave (default) / from two frames per workgroup), "rounds" (block-shared streamer
- * band count in rounds of resident workgroups, 0 = 6), "tail" (its XCD tail split), "prefetch",
- * "ratio_prefetch", "ryx_split", "ryx_adj", "ryx_cpt", "ryx_uc", "ryg_cpt", "stream_variant", "lanes",
- * "chunk_frames", "host_stage" (A/B of kernel variants and schedules, see libiqo_amd/csrc/abi.hip; round 5 removed
- * "lin_prefetch", "ratio_alt", "ring_pack" and "xcd_order", which no default used).  Every option changes speed only,
- * never the output bytes.  IQO_HIP_EINVAL for an unknown key or value. */
+/* Options: "force_general" (0/1: every shape through IQO_KERNEL_GENERAL), "bands" (row bands per
+ * frame, 0 = auto) and "host_stage" (host-pointer path of frames >= 4 MiB: 0 the HIP runtime's own
+ * pageable copies (default), 1 the pinned-staging band pipeline).  Every option changes speed
+ * only, never the output bytes.  IQO_HIP_EINVAL for an unknown key or value.
+ * With IQO_HIP_TUNING=1 in the environment the call also takes the A/B keys of
+ * libiqo_amd/csrc/abi.hip (kernel family switches "tile", "walk", "up2", "d32", "a32", "u23",
+ * "l23", "d31", "ryx", "ryg"; schedules "tile_rows", "stack", "rounds", "tail", "prefetch",
+ * "ratio_prefetch", "ryx_split", "ryx_adj", "ryx_cpt", "ryx_uc", "ryg_cpt", "stream_variant",
+ * "lanes", "chunk_frames"), which the tests and tuning scripts use; they are not part of the
+ * supported interface. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);
 
 /* Drop-in resize with HOST pointers (byte strides), synchronous: H2D, kernels, D2H. */

@@ -511,6 +511,9 @@ int upload_exact(iqo_hip_plan *h)
     if (h->ryx.ok && ryx_dev(h).parts == 0)
         h->ryx = iqo_amd::RyxTables();  // no column split fits the workgroup limits
     if (h->ryx.ok && h->ryx.general) {
+        // ryg_kernel reads the records of rows up to y1 - 1 + kRygPD + 1 unclamped (its FIFO look-ahead
+        // and the next row's record): build_ryg's padding must cover them
+        static_assert(iqo_amd::kRygRecPad >= iqo_amd::kRygPD + 2, "ryg row records: padding below the look-ahead");
         std::vector<int4> rr(h->ryx.rowRec.size() / 2);
         for (size_t i = 0; i < rr.size(); ++i) {
             const size_t ia = std::min(rr.size() - 1, i + iqo_amd::kRygPD - 1);  // (rows past the end repeat)
@@ -1500,6 +1503,16 @@ int iqo_hip_plan_prepare(iqo_hip_plan *h)
     return ensure_tables(h);
 }
 
+// The A/B keys (kernel family switches, band / lane / prefetch / column-split schedules; every one
+// speed-only) are accepted only with IQO_HIP_TUNING=1 in the environment -- tests, bench.py
+// --option and the tuning scripts set it; a caller of the public ABI sees force_general, bands and
+// host_stage only (include/iqo_hip.h).
+bool tuning_enabled()
+{
+    const char *e = std::getenv("IQO_HIP_TUNING");
+    return e && *e && std::strcmp(e, "0") != 0;
+}
+
 int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
 {
     if (!h || !key)
@@ -1508,6 +1521,20 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->forceGeneral = value != 0;
         return IQO_HIP_OK;
     }
+    if (!std::strcmp(key, "bands")) {
+        if (value < 0)
+            return IQO_HIP_EINVAL;
+        h->bands = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "host_stage")) {  // host-pointer path of large frames (speed only): 0 the runtime's
+        if (value < 0 || value > 1)              // pageable copies, 1 the pinned staging pipeline
+            return IQO_HIP_EINVAL;
+        h->hostStage = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!tuning_enabled())
+        return IQO_HIP_EINVAL;
 #ifdef IQO_VARIANT_DEBUG
     if (!std::strcmp(key, "debug_flags")) {  // variant builds only: timing experiments, wrong results
         h->debugFlags = static_cast<int>(value);
@@ -1620,12 +1647,6 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         h->ratioPrefetch = static_cast<int>(value);
         return IQO_HIP_OK;
     }
-    if (!std::strcmp(key, "host_stage")) {  // host-pointer path of large frames (speed only): 0 the runtime's
-        if (value < 0 || value > 1)              // pageable copies, 1 the pinned staging pipeline
-            return IQO_HIP_EINVAL;
-        h->hostStage = static_cast<int>(value);
-        return IQO_HIP_OK;
-    }
     if (!std::strcmp(key, "ryg")) {  // 0: general-row downscales (1 .. 2 : 1) use the wave walker / tile kernel
         h->useRyg = value != 0;
         return IQO_HIP_OK;
@@ -1650,12 +1671,6 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         if (value < 0)
             return IQO_HIP_EINVAL;
         h->chunkFrames = static_cast<int>(value);
-        return IQO_HIP_OK;
-    }
-    if (!std::strcmp(key, "bands")) {
-        if (value < 0)
-            return IQO_HIP_EINVAL;
-        h->bands = static_cast<int>(value);
         return IQO_HIP_OK;
     }
     return IQO_HIP_EINVAL;
@@ -1850,9 +1865,12 @@ static int host_resize(iqo_hip_plan *h, HostStage *st, size_t srcSt, const uint8
     // small frames are always staged: the pinned-memory queries cost more than the copy
     const bool small = sBytes < kHostPipeMinBytes;
     const bool pinSrc = !small && is_pinned_host(src), pinDst = !small && is_pinned_host(dst);
-    if (!pinSrc && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
+    // pinned staging: the small-frame path and the banded pipeline (host_stage = 1) use it; the
+    // default large-frame path (host_direct) copies straight from the caller's buffers
+    const bool staged = small || h->hostStage;
+    if (staged && !pinSrc && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
         return IQO_HIP_ENOMEM;
-    if (!pinDst && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
+    if (staged && !pinDst && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
         return IQO_HIP_ENOMEM;
 
     const int dstH = p.dstH;
@@ -2105,9 +2123,12 @@ int iqo_hip_resize_yuv420(iqo_hip_yuv_plan *yp, size_t srcStY, const uint8_t *sr
         rc = IQO_HIP_ENOMEM;
     const bool pinY = is_pinned_host(srcY), pinU = is_pinned_host(srcU), pinV = is_pinned_host(srcV);
     const bool pinYd = is_pinned_host(dstY), pinUd = is_pinned_host(dstU), pinVd = is_pinned_host(dstV);
-    if (!rc && !(pinY && pinU && pinV) && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
+    // (pinned staging only for the banded pipeline, host_stage = 1: host_direct copies straight
+    // from the caller's buffers)
+    const bool staged = yp->y->hostStage != 0;
+    if (!rc && staged && !(pinY && pinU && pinV) && grow_pinned(&st->hSrc, &st->hSrcCap, sBytes))
         rc = IQO_HIP_ENOMEM;
-    if (!rc && !(pinYd && pinUd && pinVd) && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
+    if (!rc && staged && !(pinYd && pinUd && pinVd) && grow_pinned(&st->hDst, &st->hDstCap, dBytes))
         rc = IQO_HIP_ENOMEM;
     if (!rc) {
         HostPlane pl[3] = {{yp->y, srcStY, srcY, dstStY, dstY, 0, 0, sY, dY, pinY, pinYd},

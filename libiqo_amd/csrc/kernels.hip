@@ -1437,7 +1437,9 @@ __device__ __forceinline__ void lanczos_symb_kernel_body(const LanczosArgs &a, c
 
     uint4 n0, n1;  // this iteration's two new rows (read from LDS one iteration ahead)
     wait_vmcnt<WAIT>();
-    asm volatile("" ::: "memory");
+    // the zero pads above are ds_writes that other waves' left halo lanes read: publish them
+    // explicitly (as every LDS-publishing barrier since round 5's race fix)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     read_iter(0, n0, n1);

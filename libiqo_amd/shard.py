@@ -140,18 +140,19 @@ def gather_ops(sh, src, src_fst, src_pitch, frames, dst, dst_fst, dst_pitch, wid
 class HipBandBackend:
     """Row-band shards on gfx950 devices through the C ABI.
 
-    `src` holds the whole source batch (uint8 torch tensor [F, srcH, srcSt]) on device
-    `src_device`, or in (pinned) host memory when src_device < 0; `out` [F, dstH, dstSt] is the
+    `src` holds the source batch (uint8 torch tensor [F, rows, srcSt]: source rows [src_row0,
+    src_row0 + rows) of every frame -- the whole frame, or only the windows this process scatters)
+    on device `src_device`, or in (pinned) host memory when src_device < 0; `out` [F, dstH, dstSt] is the
     output batch on `out_device` (the root; in the distributed drive only rank 0 needs it).
     Each shard gets its window by iqo_hip_copy_frames (peer DMA over xGMI, or H2D), runs
     iqo_hip_resize_band on its device's current stream, and its band goes back by
     iqo_hip_copy_frames (local drive) or by IPC handle + peer copy (distributed drive)."""
 
-    def __init__(self, make_resizer, src, src_device, out, out_device):
+    def __init__(self, make_resizer, src, src_device, out, out_device, src_row0=0):
         import torch
 
         self.torch = torch
-        self.src, self.src_device = src, src_device
+        self.src, self.src_device, self.src_row0 = src, src_device, src_row0
         self.out, self.root = out, out_device
         self.frames = src.shape[0]
         self.src_st, self.src_fst = src.stride(1), src.stride(0)
@@ -178,9 +179,12 @@ class HipBandBackend:
         from . import copy_frames
 
         rows = sh.s1 - sh.s0
+        if sh.s0 < self.src_row0 or sh.s1 > self.src_row0 + self.src.shape[1]:
+            raise ValueError("shard window rows [%d, %d) outside the source rows held [%d, %d)" %
+                             (sh.s0, sh.s1, self.src_row0, self.src_row0 + self.src.shape[1]))
         win = self.torch.empty((self.frames, rows, self.src_st), dtype=self.torch.uint8, device=self._dev(sh.device))
         stream = self.torch.cuda.current_stream(self._dev(sh.device))
-        base = self.src.data_ptr() + sh.s0 * self.src_st
+        base = self.src.data_ptr() + (sh.s0 - self.src_row0) * self.src_st
         p = copy_frames(win.data_ptr(), sh.device, win.stride(0), base, self.src_device, self.src_fst,
                         rows * self.src_st, self.frames, stream)
         self._route("scatter", p)

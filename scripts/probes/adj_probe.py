@@ -2,6 +2,7 @@
 """Find where a 2:1 ryx column mode differs from the oracle (GPU box tooling)."""
 import sys
 import os
+os.environ.setdefault("IQO_HIP_TUNING", "1")  # A/B option keys (include/iqo_hip.h)
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))

@@ -2,6 +2,7 @@
 """Compare 2:1 ryx column modes against each other on whole batches, repeatedly (GPU box tooling)."""
 import sys
 import os
+os.environ.setdefault("IQO_HIP_TUNING", "1")  # A/B option keys (include/iqo_hip.h)
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import torch

@@ -20,6 +20,7 @@ bit against the oracle after the timing.
 import argparse
 import json
 import os
+os.environ.setdefault("IQO_HIP_TUNING", "1")  # A/B option keys (include/iqo_hip.h)
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

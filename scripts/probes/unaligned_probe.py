@@ -2,6 +2,7 @@
 """Do unaligned dword buffer loads work on this GPU?  ryx / ryg on a source whose base and row stride
 are not 4-byte aligned (option unaligned_src), compared with the oracle (GPU box tooling)."""
 import os
+os.environ.setdefault("IQO_HIP_TUNING", "1")  # A/B option keys (include/iqo_hip.h)
 import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)

@@ -8,6 +8,7 @@ Output: one line per shape (profiles/r05/ratio_sweep.txt).
 """
 import argparse
 import os
+os.environ.setdefault("IQO_HIP_TUNING", "1")  # A/B option keys (include/iqo_hip.h)
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -8,6 +8,9 @@ ROOT = os.path.dirname(HERE)
 for p in (HERE, ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
+# the tests exercise every kernel family and schedule through the A/B option keys, which the
+# library accepts only with IQO_HIP_TUNING set (include/iqo_hip.h iqo_hip_plan_set_option)
+os.environ.setdefault("IQO_HIP_TUNING", "1")
 
 
 def pytest_configure(config):

@@ -37,7 +37,8 @@ uint8_t edge_div(int s, uint32_t m, int t)
 
 extern "C" {
 
-// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23, 4 = linear_u23, 5 = lanczos_d31, 6 = ryx, 7 = linear_d2.  Returns 0 on success, 1 if the shape is
+// kind: 0 = lanczos_d32, 1 = lanczos_up2, 2 = area_d32, 3 = lanczos_u23, 4 = linear_u23, 5 = lanczos_d31, 6 = ryx, 7 = linear_d2,
+// 8 = linear_up2, 9 = ryg.  Returns 0 on success, 1 if the shape is
 // not eligible for that kernel, -1 on bad arguments.
 int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int dstW, int dstH, int pxScale,
                const uint8_t *src, uint8_t *dst)
@@ -275,6 +276,62 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
             }
         }
         return 0;
+    }
+    if (kind == 9) {
+        // ryg_kernel (general rows, plan.cpp build_ryg): output row y takes the TK taps from rowRec
+        // {first window row s(y), coefficient offset c(y)}; rows outside the image read as zero; masked
+        // Lanczos border rows divided by ydiv2; columns as ryx.  The kernel reads the records of rows
+        // up to y + 2 and, through them, s(y + 2 + kPD - 1) unclamped past the last row (its FIFO
+        // look-ahead, kernels.hip ryg_kernel / abi.hip): read them here too, so a sanitizer build
+        // catches a record table shorter than that (kRygRecPad)
+        RyxTables r;
+        build_ryg(p, &r);
+        if (!r.ok)
+            return 1;
+        constexpr int kPD = 4;  // kernels.hpp kRygPD (IQO_RYG_PD)
+        const bool lz = method == 0;
+        const int TK = r.taps, NP = r.NP;
+        const size_t nRec = r.rowRec.size() / 2;
+        int64_t touch = 0;
+        std::vector<uint16_t> wrow(static_cast<size_t>(srcW + 2 * kRyxPad), 0);
+        for (int y = 0; y < dstH; ++y) {
+            const int s0 = r.rowRec.at(static_cast<size_t>(2 * y)), co = r.rowRec.at(static_cast<size_t>(2 * y + 1));
+            touch += r.rowRec.at(static_cast<size_t>(2 * (y + 2))) + r.rowRec.at(static_cast<size_t>(2 * (y + 2 + kPD - 1)));
+            if (static_cast<size_t>(y + 2 + kPD - 1) >= nRec)
+                return -2;
+            for (int c = 0; c < srcW; ++c) {
+                uint16_t acc = 0;
+                for (int k = 0; k < TK; ++k)
+                    acc = static_cast<uint16_t>(acc + px(s0 + k, c) * static_cast<uint16_t>(r.rowCoef.at(static_cast<size_t>(co + k))));
+                if (lz && (y < r.m0 || y >= r.m1)) {
+                    const int side = y < r.m0 ? 0 : 1, bi = side ? y - r.m1 : y;
+                    acc = ydiv1(acc, r.yM[side][bi < 0 ? 0 : bi > 15 ? 15 : bi], r.yS[side][bi < 0 ? 0 : bi > 15 ? 15 : bi]);
+                }
+                wrow[static_cast<size_t>(kRyxPad + c)] = acc;
+            }
+            for (int x = 0; x < dstW; ++x) {
+                const int32_t *cx = &r.cols.at(static_cast<size_t>(x) * 4);
+                const int a = cx[0] / 2;
+                int64_t sum = lz ? (1 << 19) : (1 << 22);
+                for (int q = 0; q < NP; ++q) {
+                    const uint32_t c = r.colCoef.at(static_cast<size_t>(x) * NP + q);
+                    const uint16_t w0 = wrow.at(static_cast<size_t>(a + 2 * q)), w1 = wrow.at(static_cast<size_t>(a + 2 * q + 1));
+                    if (lz)
+                        sum += static_cast<int16_t>(w0) * static_cast<int16_t>(c & 0xffffu) + static_cast<int16_t>(w1) * static_cast<int16_t>(c >> 16);
+                    else
+                        sum += static_cast<int64_t>(w0) * (c & 0xffffu) + static_cast<int64_t>(w1) * (c >> 16);
+                }
+                uint8_t o;
+                if (lz) {
+                    o = edge_div(static_cast<int>(sum), static_cast<uint32_t>(cx[1]), cx[2]);
+                } else {
+                    const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(static_cast<uint32_t>(sum)) >> 23));
+                    o = static_cast<uint8_t>(u > 255 ? 255 : u);
+                }
+                dst[static_cast<size_t>(y) * dstW + x] = o;
+            }
+        }
+        return touch == -1 ? -3 : 0;  // (keeps the look-ahead reads)
     }
     if (kind == 7) {
         // linear_d2_body (Linear 2:1 through IQO_KERNEL_AREA_INT): main rows / columns blend

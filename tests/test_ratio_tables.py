@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
 KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6, "linear_up": 8,
-         "linear_d2": 7}
+         "linear_d2": 7, "ryg": 9}
 
 
 @pytest.fixture(scope="module")
@@ -90,7 +90,14 @@ def _shapes():
            ("ryx", "lanczos", 9, 3840, 2160, 1920, 1080), ("ryx", "lanczos", 9, 5120, 64, 2560, 32),
            ("ryx", "lanczos", 3, 640, 480, 1920, 1080), ("ryx", "lanczos", 2, 640, 480, 1920, 1080),  # 4:9 up
            ("ryx", "lanczos", 3, 720, 480, 1620, 1080), ("ryx", "lanczos", 3, 320, 240, 720, 540),
-           ("ryx", "lanczos", 2, 64, 16, 100, 36)]
+           ("ryx", "lanczos", 2, 64, 16, 100, 36),
+           # general rows (ryg): 1..2:1, 2..3:1 (NL 3), 3..4:1 (NL 4), upscale rows (NL 1), Area / Linear
+           ("ryg", "lanczos", 3, 1920, 1080, 1366, 768), ("ryg", "area", 0, 1920, 1080, 1366, 768),
+           ("ryg", "linear", 0, 1920, 1080, 1366, 768), ("ryg", "lanczos", 2, 1920, 1080, 1024, 576),
+           ("ryg", "lanczos", 3, 1024, 576, 1920, 1080), ("ryg", "lanczos", 3, 1366, 768, 1920, 1080),
+           ("ryg", "lanczos", 3, 3840, 2160, 1366, 768), ("ryg", "lanczos", 3, 3840, 2160, 1024, 576),
+           ("ryg", "area", 0, 3840, 2160, 1366, 768), ("ryg", "lanczos", 4, 1024, 576, 1920, 1080),
+           ("ryg", "lanczos", 3, 1367, 769, 1920, 1080), ("ryg", "lanczos", 2, 1918, 1078, 1366, 768)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -109,6 +116,11 @@ def _shapes():
                     2 * rng.randint(sw // 4 + 1, min(1024, sw - 2) // 2) - rng.randint(0, 1), 4 * b + 16))
         out.append(("ryx", "lanczos", rng.choice((1, 4, 5, 6, 7, 8, 9)), sw, 2 * b + 40, sw // 2, b + 20))
         out.append(("ryx", "lanczos", rng.choice((2, 3)), 4 * sw, 4 * b + 40, sw, b + 10))
+        # general rows: a random row ratio in (1, 2), (2, 3) or upscaled, columns by about the same
+        hr = rng.choice((1.2, 1.45, 1.8, 2.5, 0.7, 0.55))
+        gh = 8 * rng.randint(8, 40)
+        out.append(("ryg", rng.choice(("lanczos", "area")) if hr > 1 else "lanczos", rng.choice((2, 3)), sw, gh,
+                    max(16, int(sw / hr) & ~1), max(8, int(gh / hr))))
         uw = sw // 2 & ~3  # 4:9 rows, columns upscaled (<= 4 coefficient pairs)
         out.append(("ryx", "lanczos", rng.choice((2, 3)), uw, 4 * b + 16, rng.randint(uw, min(4096, 3 * uw)), 9 * b + 36))
     return out

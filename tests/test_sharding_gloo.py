@@ -206,3 +206,43 @@ def test_bench_spawns_one_rank_per_gpu(n):
     d = json.loads(lines[0])
     assert d["world_size"] == n and d["rank_sum"] == n * (n - 1) / 2
     assert sorted(x["local_rank"] for x in d["ranks"]) == list(range(n))
+
+
+class _HostBandResizer:
+    """Stand-in for a libiqo_amd resizer in bench.band_buffers: srcH and the host band window
+    (iqo_hip_band_src_rows' host twin), no device."""
+
+    def __init__(self, case):
+        self.m, self.d, self.srcW, self.srcH, self.dstW, self.dstH, self.px = case
+
+    def band_src_rows(self, r0, n):
+        return libiqo_amd.host_band_src_rows(self.m, self.d, self.srcW, self.srcH, self.dstW, self.dstH, self.px, r0, n)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_bench_band_buffers_are_bounded_by_the_rank_window(world):
+    """in --shard band every rank held the whole global batch (pageable and
+    pinned).  bench.band_buffers allocates only the rank's own source window (shard.band_plan) and
+    its band, and the window's rows equal the same rows of the per-frame-seeded global frames."""
+    import torch
+
+    import bench
+    case = ("lanczos", 3, 384, 216, 192, 108, 1)
+    rz = _HostBandResizer(case)
+    frames, rot = 5, 2
+    plan = shard.band_plan(rz, rz.dstH, world)
+    for rank in range(world):
+        r0, r1, s0, s1 = plan[rank]
+        for src_kind in ("device", "host"):
+            mine, host, wins, bands, got_rot = bench.band_buffers(rz, frames, rz.srcW, rz.dstW, rz.dstH, rank, world,
+                                                                  "cpu", src_kind, rot)
+            assert (mine.r0, mine.r1, mine.s0, mine.s1) == (r0, r1, s0, s1) and got_rot == rot
+            win = host if src_kind == "host" else wins[0]
+            assert tuple(win.shape) == (frames, s1 - s0, rz.srcW)  # the window, not [frames, srcH, srcW]
+            assert (len(wins), host is None) == ((0, False) if src_kind == "host" else (1, True))
+            assert len(bands) == rot and all(tuple(b.shape) == (frames, r1 - r0, rz.dstW) for b in bands)
+            window_bytes = frames * ((s1 - s0) * rz.srcW + (r1 - r0) * rz.dstW)
+            held = sum(t.numel() for t in wins + bands) + (host.numel() if host is not None else 0)
+            assert held <= rot * window_bytes < frames * rz.srcH * rz.srcW * rot or world == 1
+            for f in (0, frames - 1):  # frame f's window rows = rows [s0, s1) of frame f
+                assert torch.equal(win[f], bench.band_frame(f, rz.srcH, rz.srcW, "cpu")[s0:s1])
