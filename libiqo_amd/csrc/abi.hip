@@ -88,6 +88,13 @@ struct iqo_hip_plan {
     int4 *dRyxCols = nullptr;
     int4 *dRyxRowRec = nullptr;  // general-row tables (ryx.general: the ryg kernel, kernels.hpp RygDev)
     bool useRyg = true;
+    // general upscale rows by window position (kernels.hip ryu_kernel): records, first window start
+    int4 *dRyuPos = nullptr;
+    int ryuBase = 0;
+    bool hasRyu = false;  // the table exists (every window position holds 1 or 2 rows)
+    bool useRyu = true;   // option "ryu" = 0: ryg_kernel's NL = 1 mode instead (A/B)
+    uint32_t *dRyuRun = nullptr;  // run-mode column table (plan.hpp colRun), when it exists
+    bool useRyuRun = true;        // option "ryu_run" = 0: per-column mode (A/B)
     int hostStage = 0;  // host-pointer path, frames >= 4 MiB: 0 the runtime's own pageable copies, 1 our pinned
                         // staging pipeline (host_pipeline), for A/B
     bool useD32 = true;
@@ -496,6 +503,24 @@ std::vector<int4> coord_records(const AxisPlan &a)
 // Upload the separable tile kernel's tables (TileRec / TileCol have the int4 / int2 layout).
 iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h);
 
+// Window-position records of a general upscale (plan.cpp build_ryu_positions, kernels.hip
+// ryu_kernel); none when a position holds more than 2 rows: ryg_kernel's NL = 1 mode runs the plan.
+int ryu_positions(iqo_hip_plan *h)
+{
+    h->hasRyu = iqo_amd::build_ryu_positions(h->p.dstH, &h->ryx);
+    if (!h->hasRyu)
+        return IQO_HIP_OK;
+    static_assert(iqo_amd::kRyuPosPad >= 3, "ryu_kernel reads the records up to a band's last position + 2");
+    h->ryuBase = h->ryx.posBase;
+    std::vector<int4> pos(h->ryx.posRec.size() / 4);
+    for (size_t i = 0; i < pos.size(); ++i)
+        pos[i] = make_int4(h->ryx.posRec[4 * i], h->ryx.posRec[4 * i + 1], h->ryx.posRec[4 * i + 2], h->ryx.posRec[4 * i + 3]);
+    int rc = upload(h, &h->dRyuPos, pos.data(), pos.size());
+    if (!rc && iqo_amd::build_ryu_runs(h->p.dstW, &h->ryx))
+        rc = upload(h, &h->dRyuRun, h->ryx.colRun.data(), h->ryx.colRun.size());
+    return rc;
+}
+
 // Tables of the exact-ratio kernels (most take their coefficients as kernel arguments; ryx has
 // device tables).  Built whether or not the tile tables exist: ryx also serves shapes whose taps
 // exceed the tile kernel's (Lanczos-8/9 2:1).
@@ -522,6 +547,11 @@ int upload_exact(iqo_hip_plan *h)
         const int rc2 = upload(h, &h->dRyxRowRec, rr.data(), rr.size());
         if (rc2)
             return rc2;
+        if (h->ryx.rowLoads == 1) {
+            const int rc3 = ryu_positions(h);
+            if (rc3)
+                return rc3;
+        }
     }
     if (h->ryx.ok) {
         std::vector<int4> rc(h->ryx.cols.size() / 4);
@@ -638,6 +668,8 @@ void reset_options(iqo_hip_plan *h)
     h->chunkFrames = 0;
     h->useTile = h->useWalk = h->useUp2 = h->useD32 = h->useD31 = h->useRyx = h->useL23 = h->useU23 = h->useA32 = true;
     h->useRyg = true;
+    h->useRyu = true;
+    h->useRyuRun = true;
     h->hostStage = 0;
     if (h->tt.ok) {  // option "tile_rows"
         h->tt.TH = h->tileTH0;
@@ -1134,6 +1166,18 @@ iqo_amd::RygDev ryg_dev(const iqo_hip_plan *h)
     std::memcpy(d.ce, x.ce, sizeof d.ce);
     d.cpt = x.cpt;
     d.nl = h->ryx.rowLoads;
+    if (d.nl == 1 && h->hasRyu && h->useRyu) {
+        d.posRec = h->dRyuPos;
+        d.posBase = h->ryuBase;
+        // run mode: 4 adjacent columns per thread, every part starting on a multiple of 4 columns
+        bool aligned = d.cpt == 4 && h->ryx.runPairs > 0 && h->useRyuRun;
+        for (int k = 0; k < d.parts && aligned; ++k)
+            aligned = d.xs[k] % 4 == 0;
+        if (aligned) {
+            d.colRun = h->dRyuRun;
+            d.run = h->ryx.runPairs;
+        }
+    }
     return d;
 }
 
@@ -1649,6 +1693,14 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
     }
     if (!std::strcmp(key, "ryg")) {  // 0: general-row downscales (1 .. 2 : 1) use the wave walker / tile kernel
         h->useRyg = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryu_run")) {  // 0: general upscale rows read each column's window separately
+        h->useRyuRun = value != 0;
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "ryu")) {  // 0: general upscale rows walk output rows (ryg_kernel NL = 1), not window positions
+        h->useRyu = value != 0;
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "ryx")) {  // 0: exact-vertical-ratio downscales use the general kernels

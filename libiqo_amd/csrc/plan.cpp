@@ -1705,6 +1705,78 @@ void build_ryg(const Plan &p, RyxTables *t)
     t->ok = true;
 }
 
+bool build_ryu_positions(int dstH, RyxTables *t)
+{
+    t->posRec.clear();
+    t->posBase = 0;
+    if (!t->ok || !t->general || t->rowLoads != 1 || dstH < 1 || t->rowRec.size() < static_cast<size_t>(2 * dstH))
+        return false;
+    std::vector<int32_t> pos;
+    const int32_t s0 = t->rowRec[0];
+    for (int y = 0; y < dstH; ++y) {
+        const int32_t s = t->rowRec[static_cast<size_t>(2 * y)], c = t->rowRec[static_cast<size_t>(2 * y + 1)];
+        const int64_t k = static_cast<int64_t>(s) - s0, n = static_cast<int64_t>(pos.size() / 4);
+        if (k == n) {
+            pos.insert(pos.end(), {y, 1, c, c});
+        } else if (k == n - 1 && pos[pos.size() - 3] == 1) {
+            pos[pos.size() - 3] = 2;
+            pos[pos.size() - 1] = c;
+        } else {
+            return false;  // a position of 3 rows, or a window that moved back or skipped a row
+        }
+    }
+    const int32_t lastC = pos.back();
+    for (int k = 0; k < kRyuPosPad; ++k)
+        pos.insert(pos.end(), {dstH, 1, lastC, lastC});
+    t->posRec = std::move(pos);
+    t->posBase = s0;
+    return true;
+}
+
+bool build_ryu_runs(int dstW, RyxTables *t)
+{
+    t->colRun.clear();
+    t->runPairs = 0;
+    const int NP = t->NP;
+    if (!t->ok || NP < 1 || dstW < 1 || t->cols.size() < static_cast<size_t>(4 * dstW) ||
+        t->colCoef.size() < static_cast<size_t>(NP) * dstW)
+        return false;
+    // dword offset of each column's window in its group's run (from the lowest even start of the
+    // group: a phase-0 column's window is trimmed to its one nonzero tap, so the starts are not
+    // monotonic), and the pairs the run must hold
+    std::vector<int> off(static_cast<size_t>(dstW));
+    int need = 0;
+    for (int x = 0; x < dstW; ++x) {
+        int lo = t->cols[static_cast<size_t>(4 * x)];
+        for (int k = x & ~3; k < std::min(dstW, (x & ~3) + 4); ++k)
+            lo = std::min(lo, t->cols[static_cast<size_t>(4 * k)]);
+        const int d = t->cols[static_cast<size_t>(4 * x)] - lo;
+        if (d % 4)
+            return false;
+        off[static_cast<size_t>(x)] = d / 4;
+        int last = -1;  // the column's last nonzero pair
+        for (int q = 0; q < NP; ++q)
+            if (t->colCoef[static_cast<size_t>(x) * NP + q])
+                last = q;
+        need = std::max(need, d / 4 + last + 1);
+    }
+    const int R = std::max(need, NP + 1);
+    if (R > NP + 2)
+        return false;  // (kernels.hip instantiates runs of NP + 1 and NP + 2 pairs)
+    t->colRun.assign(static_cast<size_t>(dstW) * R, 0u);
+    for (int x = 0; x < dstW; ++x)
+        for (int q = 0; q < NP; ++q) {
+            const int r = off[static_cast<size_t>(x)] + q;
+            const uint32_t c = t->colCoef[static_cast<size_t>(x) * NP + q];
+            if (r < R)
+                t->colRun[static_cast<size_t>(x) * R + r] = c;
+            else if (c)
+                return false;
+        }
+    t->runPairs = R;
+    return true;
+}
+
 // The nonzero taps [first, last] of output column x (round 5: the column tables drop the zero taps
 // at either end of a window, e.g. Lanczos-3 1920 -> 1366 has 10-tap windows holding at most 9
 // nonzero taps: 5 pairs instead of 6)

@@ -7,6 +7,7 @@
 // multiply-high edge division, v_ashr_pk_u8_i32 saturation.  Never part of the product.
 #include "plan.hpp"
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -332,6 +333,83 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
             }
         }
         return touch == -1 ? -3 : 0;  // (keeps the look-ahead reads)
+    }
+    if (kind == 10 || kind == 11) {
+        // ryu_kernel (general upscale rows walked by window position, plan.cpp build_ryu_positions):
+        // for each band [y0, y1) the kernel takes positions pA = s(y0) .. s(y1 - 1); position p's
+        // record gives the output rows whose window starts at pA + p, clipped to the band, and their
+        // tap offsets; it reads the records of positions p + 1 and p + 2 unclamped.  Emulated over
+        // several band heights: every band plan must give the same image, every row written once.
+        RyxTables r;
+        build_ryg(p, &r);
+        if (!r.ok || !build_ryu_positions(dstH, &r))
+            return 1;
+        // kind 11: the run mode (4 adjacent columns from one run of runPairs dwords, build_ryu_runs)
+        const bool run = kind == 11;
+        if (run && !build_ryu_runs(dstW, &r))
+            return 1;
+        const bool lz = method == 0;
+        const int TK = r.taps, NP = r.NP;
+        const size_t nPosRec = r.posRec.size() / 4;
+        std::vector<uint16_t> wrow(static_cast<size_t>(srcW + 2 * kRyxPad), 0);
+        std::vector<uint8_t> first;
+        for (const int rpb : {dstH, 7, 13, 1, 64}) {
+            std::vector<int> written(static_cast<size_t>(dstH), 0);
+            for (int y0 = 0; y0 < dstH; y0 += rpb) {
+                const int y1 = std::min(dstH, y0 + rpb);
+                const int pA = r.rowRec.at(static_cast<size_t>(2 * y0));
+                const int nPos = r.rowRec.at(static_cast<size_t>(2 * (y1 - 1))) - pA + 1;
+                for (int q = 0; q < nPos; ++q) {
+                    const size_t ri = static_cast<size_t>(pA - r.posBase + q);
+                    if (ri + 2 >= nPosRec)
+                        return -2;  // the kernel's look-ahead would read past the table
+                    const int32_t *rc = &r.posRec.at(4 * ri);
+                    const int ya = std::max(rc[0], y0), cnt = std::min(rc[0] + rc[1], y1) - ya;
+                    if (cnt < 1 || cnt > 2 || (cnt == 2 && ya != rc[0]))
+                        return -4;
+                    for (int k = 0; k < cnt; ++k) {
+                        const int y = ya + k, co = k ? rc[3] : (ya == rc[0] ? rc[2] : rc[3]);
+                        ++written.at(static_cast<size_t>(y));
+                        for (int c = 0; c < srcW; ++c) {
+                            uint16_t acc = 0;
+                            for (int t2 = 0; t2 < TK; ++t2)
+                                acc = static_cast<uint16_t>(acc + px(pA + q + t2, c) *
+                                                                      static_cast<uint16_t>(r.rowCoef.at(static_cast<size_t>(co + t2))));
+                            if (lz && (y < r.m0 || y >= r.m1)) {
+                                const int side = y < r.m0 ? 0 : 1, bi = side ? y - r.m1 : y;
+                                acc = ydiv1(acc, r.yM[side][bi < 0 ? 0 : bi > 15 ? 15 : bi], r.yS[side][bi < 0 ? 0 : bi > 15 ? 15 : bi]);
+                            }
+                            wrow[static_cast<size_t>(kRyxPad + c)] = acc;
+                        }
+                        for (int x = 0; x < dstW; ++x) {
+                            const int32_t *cx = &r.cols.at(static_cast<size_t>(x) * 4);
+                            int a = cx[0] / 2;
+                            if (run)  // the group's lowest even start
+                                for (int k = x & ~3; k < std::min(dstW, (x & ~3) + 4); ++k)
+                                    a = std::min(a, r.cols.at(static_cast<size_t>(k) * 4) / 2);
+                            const int nq = run ? r.runPairs : NP;
+                            int64_t sum = 1 << 19;
+                            for (int q2 = 0; q2 < nq; ++q2) {
+                                const uint32_t c = run ? r.colRun.at(static_cast<size_t>(x) * nq + q2)
+                                                       : r.colCoef.at(static_cast<size_t>(x) * NP + q2);
+                                const uint16_t w0 = wrow.at(static_cast<size_t>(a + 2 * q2)), w1 = wrow.at(static_cast<size_t>(a + 2 * q2 + 1));
+                                sum += static_cast<int16_t>(w0) * static_cast<int16_t>(c & 0xffffu) +
+                                       static_cast<int16_t>(w1) * static_cast<int16_t>(c >> 16);
+                            }
+                            dst[static_cast<size_t>(y) * dstW + x] = edge_div(static_cast<int>(sum), static_cast<uint32_t>(cx[1]), cx[2]);
+                        }
+                    }
+                }
+            }
+            for (int y = 0; y < dstH; ++y)
+                if (written[static_cast<size_t>(y)] != 1)
+                    return -5;
+            if (first.empty())
+                first.assign(dst, dst + static_cast<size_t>(dstW) * dstH);
+            else if (!std::equal(first.begin(), first.end(), dst))
+                return -6;
+        }
+        return 0;
     }
     if (kind == 7) {
         // linear_d2_body (Linear 2:1 through IQO_KERNEL_AREA_INT): main rows / columns blend

@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
 KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6, "linear_up": 8,
-         "linear_d2": 7, "ryg": 9}
+         "linear_d2": 7, "ryg": 9, "ryu": 10, "ryu_run": 11}
 
 
 @pytest.fixture(scope="module")
@@ -97,7 +97,15 @@ def _shapes():
            ("ryg", "lanczos", 3, 1024, 576, 1920, 1080), ("ryg", "lanczos", 3, 1366, 768, 1920, 1080),
            ("ryg", "lanczos", 3, 3840, 2160, 1366, 768), ("ryg", "lanczos", 3, 3840, 2160, 1024, 576),
            ("ryg", "area", 0, 3840, 2160, 1366, 768), ("ryg", "lanczos", 4, 1024, 576, 1920, 1080),
-           ("ryg", "lanczos", 3, 1367, 769, 1920, 1080), ("ryg", "lanczos", 2, 1918, 1078, 1366, 768)]
+           ("ryg", "lanczos", 3, 1367, 769, 1920, 1080), ("ryg", "lanczos", 2, 1918, 1078, 1366, 768),
+           # general upscale rows by window position (ryu, round 6): 15:8, 45:32, Lanczos-2/4, odd sizes
+           ("ryu", "lanczos", 3, 1024, 576, 1920, 1080), ("ryu", "lanczos", 3, 1366, 768, 1920, 1080),
+           ("ryu", "lanczos", 2, 1024, 576, 1920, 1080), ("ryu", "lanczos", 4, 1024, 576, 1920, 1080),
+           ("ryu", "lanczos", 3, 1367, 769, 1920, 1080), ("ryu", "lanczos", 3, 100, 37, 130, 71),
+           ("ryu", "lanczos", 2, 64, 9, 96, 17),
+           ("ryu_run", "lanczos", 3, 1024, 576, 1920, 1080), ("ryu_run", "lanczos", 3, 1366, 768, 1920, 1080),
+           ("ryu_run", "lanczos", 4, 1024, 576, 1920, 1080), ("ryu_run", "lanczos", 2, 100, 37, 130, 71),
+           ("ryu_run", "lanczos", 3, 1367, 769, 1921, 1081)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -121,6 +129,11 @@ def _shapes():
         gh = 8 * rng.randint(8, 40)
         out.append(("ryg", rng.choice(("lanczos", "area")) if hr > 1 else "lanczos", rng.choice((2, 3)), sw, gh,
                     max(16, int(sw / hr) & ~1), max(8, int(gh / hr))))
+        uh = rng.randint(8, 200)  # upscale rows by 1 .. 2 (ryu)
+        out.append(("ryu", "lanczos", rng.choice((2, 3, 4)), sw, uh, rng.randint(sw, min(4096, 2 * sw)),
+                    rng.randint(uh + 1, 2 * uh)))
+        out.append(("ryu_run", "lanczos", rng.choice((2, 3, 4)), sw, uh, rng.randint(sw + 1, min(4096, 2 * sw)),
+                    rng.randint(uh + 1, 2 * uh)))
         uw = sw // 2 & ~3  # 4:9 rows, columns upscaled (<= 4 coefficient pairs)
         out.append(("ryx", "lanczos", rng.choice((2, 3)), uw, 4 * b + 16, rng.randint(uw, min(4096, 3 * uw)), 9 * b + 36))
     return out
