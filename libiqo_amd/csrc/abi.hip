@@ -49,6 +49,9 @@ struct iqo_hip_plan {
     bool forceGeneral = false;
     int bands = 0;
     int debugFlags = 0;
+#ifdef IQO_VARIANT_DEBUG
+    uint64_t traceAddr = 0;  // variant builds: workgroup timeline buffer of the block-shared streamer
+#endif
     int prefetch = 3;  // streamer prefetch: ring streamer depth 1..3 / symmetric LDS ring K = 3..5
     int streamVariant = 0;  // 0: block-shared symmetric streamer where eligible, 1: accumulator-ring
                             // streamer, 2: per-wave symmetric streamer (all bit-identical)
@@ -823,6 +826,9 @@ iqo_amd::LanczosDev lanczos_dev(const iqo_hip_plan *h)
     l.yBotNeg = f.yBotNeg;
     l.xNeg = f.xNeg;
     l.dbg = h->debugFlags;
+#ifdef IQO_VARIANT_DEBUG
+    l.trace = h->traceAddr;
+#endif
     l.prefetch = h->prefetch;
     l.rounds = h->rounds;
     l.tail = h->tail;
@@ -1582,6 +1588,10 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
 #ifdef IQO_VARIANT_DEBUG
     if (!std::strcmp(key, "debug_flags")) {  // variant builds only: timing experiments, wrong results
         h->debugFlags = static_cast<int>(value);
+        return IQO_HIP_OK;
+    }
+    if (!std::strcmp(key, "trace_addr")) {  // variant builds only: device buffer of 16 B per workgroup
+        h->traceAddr = static_cast<uint64_t>(value);
         return IQO_HIP_OK;
     }
 #endif

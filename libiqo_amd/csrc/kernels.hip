@@ -1409,7 +1409,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 12 ? 2
         by = lg / bands;
         bx = lg - by * bands;
     }
+#ifdef IQO_VARIANT_DEBUG
+    // workgroup timeline (variant builds): wave 0 records its start and end on the 100 MHz clock and
+    // where it ran (HW_ID: wave slot / SIMD / CU / SH / SE fields; XCC_ID), one 16-byte vector store
+    // (profiles/r06/wgtrace.txt)
+    uint32_t t0 = 0;
+    if (a.l.trace && threadIdx.x < 64)
+        t0 = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+#endif
     lanczos_symb_kernel_body<NY, NX, OFFX, K, CPW, C0ONE, LINE>(a, bx, by, rpb);
+#ifdef IQO_VARIANT_DEBUG
+    if (a.l.trace && threadIdx.x == 0) {
+        const uint32_t t1 = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+        const uint32_t hw = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(4 | (31 << 11)));   // HW_REG_HW_ID
+        const uint32_t xcc = static_cast<uint32_t>(__builtin_amdgcn_s_getreg(20 | (31 << 11))); // HW_REG_XCC_ID
+        uint4 *rec = reinterpret_cast<uint4 *>(a.l.trace) + (blockIdx.x + gridDim.x * blockIdx.y);
+        *rec = make_uint4(t0, t1, hw, xcc);
+    }
+#endif
 }
 
 

@@ -243,6 +243,11 @@ struct LanczosDev {
     // lanes' 8 exact divisions per side (5 border columns: left lane k < 8, right lane k >= 8,
     // identity in the interior) as multipliers in cx[0 .. 16) (the ring streamer's padded table)
     // and shifts in xM[0 .. 8), xT[0 .. 8) (the 4-column scheme's constants)
+#ifdef IQO_VARIANT_DEBUG
+    // variant builds only: per-workgroup {start, end (100 MHz clock), HW_ID, XCC_ID} records of the
+    // block-shared streamer (scripts/probes/wg_trace.py); 0 = off.  Not in the shipped layout.
+    uint64_t trace;
+#endif
 };
 bool lanczos_stream_supported(int KY, int KX, int NY, int NXP, int offX);
 hipError_t launch_lanczos_stream(const LanczosDev &l, const Io &io, int rowBegin, int rowEnd, int bands,
