@@ -514,11 +514,9 @@ int ryu_positions(iqo_hip_plan *h)
     if (!h->hasRyu)
         return IQO_HIP_OK;
     static_assert(iqo_amd::kRyuPosPad >= 3, "ryu_kernel reads the records up to a band's last position + 2");
+    static_assert(iqo_amd::kRyuRec == 8, "ryu_kernel reads 8-int position records");
     h->ryuBase = h->ryx.posBase;
-    std::vector<int4> pos(h->ryx.posRec.size() / 4);
-    for (size_t i = 0; i < pos.size(); ++i)
-        pos[i] = make_int4(h->ryx.posRec[4 * i], h->ryx.posRec[4 * i + 1], h->ryx.posRec[4 * i + 2], h->ryx.posRec[4 * i + 3]);
-    int rc = upload(h, &h->dRyuPos, pos.data(), pos.size());
+    int rc = upload(h, &h->dRyuPos, reinterpret_cast<const int4 *>(h->ryx.posRec.data()), h->ryx.posRec.size() / 4);
     if (!rc && iqo_amd::build_ryu_runs(h->p.dstW, &h->ryx))
         rc = upload(h, &h->dRyuRun, h->ryx.colRun.data(), h->ryx.colRun.size());
     return rc;
@@ -534,6 +532,10 @@ int upload_exact(iqo_hip_plan *h)
     iqo_amd::build_d32(h->p, h->wt, &h->dt);
     iqo_amd::build_d31(h->p, &h->t31);
     iqo_amd::build_ryx(h->p, &h->ryx);
+#ifdef IQO_RYU_EXACT  // variant builds (A/B): exact-ratio upscale rows on the general-row kernels instead
+    if (h->ryx.ok && h->ryx.Q > h->ryx.P)
+        h->ryx = iqo_amd::RyxTables();
+#endif
     if (!h->ryx.ok)
         iqo_amd::build_ryg(h->p, &h->ryx);  // general rows (no exact P:Q)
     if (h->ryx.ok && ryx_dev(h).parts == 0)
@@ -1175,6 +1177,7 @@ iqo_amd::RygDev ryg_dev(const iqo_hip_plan *h)
     if (d.nl == 1 && h->hasRyu && h->useRyu) {
         d.posRec = h->dRyuPos;
         d.posBase = h->ryuBase;
+        d.posRows = h->ryx.posRows;
         // run mode: 4 adjacent columns per thread, every part starting on a multiple of 4 columns
         bool aligned = d.cpt == 4 && h->ryx.runPairs > 0 && h->useRyuRun;
         for (int k = 0; k < d.parts && aligned; ++k)

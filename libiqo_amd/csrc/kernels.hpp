@@ -166,11 +166,12 @@ struct RygDev {
     int cpt;                     // output columns per thread: 2 .. 4 (abi.hip ryx_dev)
     int nl = 2;                  // rows loaded per output row: 2 (downscales, windows 1 or 2 rows apart),
                                  // 1 (upscales, windows 0 or 1 rows apart)
-    // upscales whose window positions hold 1 or 2 output rows each (kernels.hip ryu_kernel): per
-    // window start s, record s - posBase = {first output row, rows (1, 2), tap offsets of that row
-    // and the next}, padded by plan.hpp kRyuPosPad records; null: ryg_kernel's NL = 1 mode
-    const int4 *posRec = nullptr;
+    // upscales whose window positions hold 1 .. posRows output rows each (kernels.hip ryu_kernel):
+    // per window start s, record s - posBase = {first output row, rows, tap offsets of those rows},
+    // 8 ints, padded by plan.hpp kRyuPosPad records; null: ryg_kernel's NL = 1 mode
+    const int4 *posRec = nullptr;  // (8 ints per record: two int4)
     int posBase = 0;
+    int posRows = 2;               // the most output rows a window position holds (2 or 3)
     // ryu_kernel run mode (cpt 4, parts on multiples of 4 columns): dstW x run pairs (plan.hpp colRun)
     const uint32_t *colRun = nullptr;
     int run = 0;

@@ -1498,11 +1498,12 @@ struct ct_lcm {
 // span about 2 source columns), so a row takes RUN LDS dwords per thread instead of 4 NP, each
 // column's coefficient pairs sit at their offset in a zero-padded run of RUN pairs (abi.hip
 // ryu_runs: 4 RUN dots per row instead of 4 NP), and the 4 output bytes go out as one dword.
-template <int T, int NP, int PD, int CPT, int RUN>
+template <int T, int NP, int PD, int CPT, int RUN, int KM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void ryu_kernel(RygArgs a)
 {
     static_assert(CPT >= 2 && CPT <= 4 && T >= 2, "output columns per thread");
     static_assert(RUN == 0 || (CPT == 4 && RUN >= NP), "run mode: 4 adjacent columns per thread");
+    static_assert(KM >= 2 && KM <= 6, "output rows per window position (rows grow by at most KM)");
     constexpr int NQ = RUN ? RUN : NP;  // pairs read (and dots) per column
     constexpr int NPK = (CPT + 1) / 2;
     constexpr int OOB = 0x7ff00000;
@@ -1538,10 +1539,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     // skip the vertical pass and its loads, uniformly)
     const bool srcWave = 256 * __builtin_amdgcn_readfirstlane(t >> 6) < span;
 
-    // work rows: 2 sets x 2 rows of (pad + span + pad) u16, zero padding written once
+    // work rows: 2 sets x KM rows of (pad + span + pad) u16, zero padding written once
     const int spanA = (span + 3) & ~3;
     const int pitch = PADB + 2 * spanA + PADB;
-    for (int i = t; i < 4 * (PADB / 4); i += static_cast<int>(blockDim.x)) {
+    for (int i = t; i < 2 * KM * (PADB / 4); i += static_cast<int>(blockDim.x)) {
         const int buf = i / (PADB / 4), k = i % (PADB / 4);
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + 4 * k) = 0u;
         *reinterpret_cast<uint32_t *>(lds + buf * pitch + PADB + 2 * spanA + 4 * k) = 0u;
@@ -1588,14 +1589,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
 
     // the band's window positions [pA, pA + nPos): the first and last rows' window starts
     const int pA = sld(d.rowRec, 4 * y0), nPos = sld(d.rowRec, 4 * (y1 - 1)) - pA + 1;
-    // position record {first output row yF, rows n, tap offsets of rows yF and yF + 1}
-    // (abi.hip ryu_positions pads the table by PD + 2 records past the last position)
-    const int4 *posRec = d.posRec + (pA - d.posBase);
-    // rows of the band at a position: [ya, ya + cnt), taps of the first at cA, the second at cB
-    auto rows_of = [&](int4 r, int &ya, int &cnt, int &cA) {
-        ya = max(r.x, y0);
-        cnt = min(r.x + r.y, y1) - ya;
-        cA = ya == r.x ? r.z : r.w;
+    // position record (8 ints, plan.cpp build_ryu_positions): {first output row yF, rows n, tap
+    // offsets of rows yF .. yF + 5}, padded by kRyuPosPad records past the last position.  Only a
+    // band's first position can start before the band (the band then starts inside it) and only its
+    // last one end after it (its rows are clipped)
+    const int *posRec = reinterpret_cast<const int *>(d.posRec) + 8 * (pA - d.posBase);
+    struct PosRec {
+        int yF, n, c[KM];
+    };
+    auto load_rec = [&](int q) {
+        PosRec r;
+        r.yF = sld(posRec, 8 * q);
+        r.n = sld(posRec, 8 * q + 1);
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+            r.c[j] = sld(posRec, 8 * q + 2 + j);
+        return r;
+    };
+    auto pin = [&](const PosRec &r) {
+        asm volatile("" ::"s"(r.yF), "s"(r.n));
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+            asm volatile("" ::"s"(r.c[j]));
     };
 
     uint32_t R[T][2];
@@ -1605,7 +1620,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     uint32_t F[PD];  // slot j: the row entering at position j + 1 (+ a multiple of PD)
 #pragma unroll
     for (int j = 0; j < PD; ++j)
-        F[j] = load_row(j + 1 < nPos ? pA + T + j : -(1 << 20));
+        F[j] = load_row(j + 1 < nPos ? pA + T + j : -1);
 
     // vertical pass of one output row from the window at ring offset O into work buffer b
     auto vertical = [&](auto oc, int b, int y, const uint32_t (&cy)[T]) {
@@ -1679,22 +1694,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
         }
     };
 
-    // prologue: position 0's rows into set 0
-    int4 rn = sload(posRec + 1);  // the next position's record
+    // prologue: the rows of position 0 inside the band into set 0 (the band may start inside it)
+    PosRec rn = load_rec(1);  // the next position's record
     {
-        int ya, cnt, cA;
-        rows_of(sload(posRec), ya, cnt, cA);
-        uint32_t cy[T];
+        const PosRec r0 = load_rec(0);
+        const int first = y0 - r0.yF, cnt = min(r0.yF + r0.n, y1) - y0;
         if (srcWave) {
-            coefs(cA, cy);
-            vertical(std::integral_constant<int, 0>{}, 0, ya, cy);
-            if (cnt > 1) {
-                coefs(sld(posRec, 3), cy);  // (cnt 2: the band starts at the position's first row)
-                vertical(std::integral_constant<int, 0>{}, 1, ya + 1, cy);
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                if (j < cnt) {
+                    int c = r0.c[0];
+#pragma unroll
+                    for (int q = 1; q < KM; ++q)
+                        c = first + j == q ? r0.c[q] : c;
+                    uint32_t cy[T];
+                    coefs(c, cy);
+                    vertical(std::integral_constant<int, 0>{}, j, y0 + j, cy);
+                }
             }
         }
     }
-    int4 rc = sload(posRec);  // this position's record
+    int ya = y0, cnt = min(sld(posRec, 0) + sld(posRec, 1), y1) - y0;  // this position's rows
 
     for (int base = 0; base < nPos; base += U) {
         static_for<U>([&](auto ic) {
@@ -1702,36 +1722,47 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
             const int p = base + i;
             if (p >= nPos)
                 return;  // whole workgroup
-            int ya, cnt, cA;
-            rows_of(rc, ya, cnt, cA);
             // scalar loads before the barrier (they share lgkmcnt with the LDS reads after it): the
-            // next position's taps and the record after it
-            int yn, cntn, cAn;
-            rows_of(rn, yn, cntn, cAn);
+            // next position's taps and the record after it (pinned here: otherwise the compiler sinks
+            // them past the barrier to their use in the next position's vertical pass, whose lgkmcnt
+            // wait then also waits for this position's LDS reads)
+            const int yn = rn.yF, cntn = min(rn.yF + rn.n, y1) - yn;  // (inside the band from position 1 on)
             const bool more = p + 1 < nPos;
-            uint32_t cyA[T], cyB[T];
-            coefs(cAn, cyA);
-            coefs(rn.w, cyB);
-            const int4 r2 = sload(posRec + (p + 2));
+            uint32_t cyn[KM][T];
+#pragma unroll
+            for (int j = 0; j < KM; ++j) {
+                coefs(rn.c[j], cyn[j]);
+#pragma unroll
+                for (int q = 0; q < T; ++q)
+                    asm volatile("" ::"s"(cyn[j][q]));
+            }
+            const PosRec r2 = load_rec(p + 2);
+            pin(r2);
             lds_barrier();
-            uint32_t wA[WK][NQ], wB[WK][NQ];
-            read_row(2 * S, wA);
-            if (cnt > 1)
-                read_row(2 * S + 1, wB);
+            uint32_t w[KM][WK][NQ];
+            read_row(KM * S, w[0]);
+#pragma unroll
+            for (int j = 1; j < KM; ++j)
+                if (j < cnt)
+                    read_row(KM * S + j, w[j]);
             // the row entering at position p + 1 (FIFO slot i mod PD) and that slot's reload
             const uint32_t f = F[i % PD];
-            F[i % PD] = load_row(p + 1 + PD < nPos ? pA + p + PD + T : -(1 << 20));
+            F[i % PD] = load_row(p + 1 + PD < nPos ? pA + p + PD + T : -1);
             if (more && srcWave) {
                 // position p + 1: its new source row replaces window row 0 of position p (slot i mod T)
                 widen(f, R[i % T]);
-                vertical(std::integral_constant<int, (i + 1) % T>{}, 2 * (S ^ 1), yn, cyA);
-                if (cntn > 1)
-                    vertical(std::integral_constant<int, (i + 1) % T>{}, 2 * (S ^ 1) + 1, yn + 1, cyB);
+#pragma unroll
+                for (int j = 0; j < KM; ++j)
+                    if (j < cntn)
+                        vertical(std::integral_constant<int, (i + 1) % T>{}, KM * (S ^ 1) + j, yn + j, cyn[j]);
             }
-            emit_row(wA, ya);
-            if (cnt > 1)
-                emit_row(wB, ya + 1);
-            rc = rn;
+            emit_row(w[0], ya);
+#pragma unroll
+            for (int j = 1; j < KM; ++j)
+                if (j < cnt)
+                    emit_row(w[j], ya + j);
+            ya = yn;
+            cnt = cntn;
             rn = r2;
         });
     }
@@ -2494,11 +2525,12 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
         int T, NP, cpt, nl;
         const void *kern;
         int run;  // ryu_kernel run mode: work-row dwords per 4 adjacent columns (0: off)
+        int km;   // ryu_kernel: output rows per window position (at most)
     };
 #define IQO_RYG_N(LZ_, T_, NP_, NL_)                                                                   \
-    {LZ_, T_, NP_, 2, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 2, NL_>), 0},    \
-    {LZ_, T_, NP_, 3, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 3, NL_>), 0},    \
-    {LZ_, T_, NP_, 4, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 4, NL_>), 0}
+    {LZ_, T_, NP_, 2, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 2, NL_>), 0, 0},    \
+    {LZ_, T_, NP_, 3, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 3, NL_>), 0, 0},    \
+    {LZ_, T_, NP_, 4, NL_, reinterpret_cast<const void *>(ryg_kernel<LZ_, T_, NP_, kRygPD, 4, NL_>), 0, 0}
 #define IQO_RYG(LZ_, T_, NP_) IQO_RYG_N(LZ_, T_, NP_, 2)
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
@@ -2507,41 +2539,44 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)
                                  IQO_RYG(false, 3, 2), IQO_RYG(false, 3, 3),
                                  // Lanczos downscales of 2 .. 3 : 1 (windows 2 or 3 rows apart; 2 columns per thread)
-                                 {true, 10, 6, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 10, 6, kRygPD, 2, 3>), 0},
-                                 {true, 12, 7, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 12, 7, kRygPD, 2, 3>), 0},
-                                 {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 3>), 0},
-                                 {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 3>), 0},
-                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 3>), 0},
+                                 {true, 10, 6, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 10, 6, kRygPD, 2, 3>), 0, 0},
+                                 {true, 12, 7, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 12, 7, kRygPD, 2, 3>), 0, 0},
+                                 {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 3>), 0, 0},
+                                 {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 3>), 0, 0},
+                                 {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 3>), 0, 0},
                                  // Area downscales of 2 .. 3 : 1
-                                 {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, kRygPD, 2, 3>), 0},
-                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, kRygPD, 2, 3>), 0},
+                                 {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, kRygPD, 2, 3>), 0, 0},
+                                 {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, kRygPD, 2, 3>), 0, 0},
                                  // downscales of 3 .. 4 : 1 (windows 3 or 4 rows apart)
-                                 {true, 14, 8, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 4>), 0},
-                                 {true, 16, 9, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 4>), 0},
-                                 {true, 18, 10, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 4>), 0},
-                                 {true, 20, 11, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 20, 11, kRygPD, 2, 4>), 0},
-                                 {true, 22, 12, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 12, kRygPD, 2, 4>), 0},
-                                 {true, 24, 13, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 24, 13, kRygPD, 2, 4>), 0},
-                                 {false, 5, 3, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 3, kRygPD, 2, 4>), 0},
-                                 {false, 5, 4, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 4, kRygPD, 2, 4>), 0}};
+                                 {true, 14, 8, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 4>), 0, 0},
+                                 {true, 16, 9, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 4>), 0, 0},
+                                 {true, 18, 10, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 4>), 0, 0},
+                                 {true, 20, 11, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 20, 11, kRygPD, 2, 4>), 0, 0},
+                                 {true, 22, 12, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 12, kRygPD, 2, 4>), 0, 0},
+                                 {true, 24, 13, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 24, 13, kRygPD, 2, 4>), 0, 0},
+                                 {false, 5, 3, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 3, kRygPD, 2, 4>), 0, 0},
+                                 {false, 5, 4, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 4, kRygPD, 2, 4>), 0, 0}};
 #undef IQO_RYG_N
 #undef IQO_RYG
     // upscale rows by window position (ryu_kernel): PD positions ahead (a trip of lcm(T, PD, 2))
-#define IQO_RYU(T_, NP_, PD_)                                                                          \
-    {true, T_, NP_, 2, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 2, 0>), 0},           \
-    {true, T_, NP_, 3, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 3, 0>), 0},           \
-    {true, T_, NP_, 4, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 4, 0>), 0},           \
-    {true, T_, NP_, 4, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 4, NP_ + 1>), NP_ + 1}, \
-    {true, T_, NP_, 4, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 4, NP_ + 2>), NP_ + 2}
+#define IQO_RYU_K(T_, NP_, PD_, KM_)                                                                   \
+    {true, T_, NP_, 2, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 2, 0, KM_>), 0, KM_},  \
+    {true, T_, NP_, 3, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 3, 0, KM_>), 0, KM_},  \
+    {true, T_, NP_, 4, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 4, 0, KM_>), 0, KM_},  \
+    {true, T_, NP_, 4, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 4, NP_ + 1, KM_>), NP_ + 1, KM_}, \
+    {true, T_, NP_, 4, 1, reinterpret_cast<const void *>(ryu_kernel<T_, NP_, PD_, 4, NP_ + 2, KM_>), NP_ + 2, KM_}
+#define IQO_RYU(T_, NP_, PD_) IQO_RYU_K(T_, NP_, PD_, 2), IQO_RYU_K(T_, NP_, PD_, 3)
     static const Inst kUp[] = {IQO_RYU(4, 3, 4), IQO_RYU(6, 4, 3), IQO_RYU(8, 5, 4)};
 #undef IQO_RYU
+#undef IQO_RYU_K
     const void *kern = nullptr;
     const bool byPos = d.nl == 1 && d.posRec;
     for (const Inst &k : kInst)
         if (!byPos && k.lz == d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt && k.nl == d.nl)
             kern = k.kern;
     for (const Inst &k : kUp)
-        if (byPos && d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt && k.run == (d.colRun ? d.run : 0))
+        if (byPos && d.lanczos && k.T == d.taps && k.NP == d.NP && k.cpt == d.cpt && k.run == (d.colRun ? d.run : 0) &&
+            k.km == std::max(2, d.posRows))
             kern = k.kern;
     if (!kern || d.parts < 1 || d.parts > 16)
         return iqo_ryg_einval(3);
@@ -2562,7 +2597,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     } else if (d.srcW > 4 * threads || d.dstW > d.cpt * threads) {
         return iqo_ryg_einval(7);
     }
-    const int ldsBytes = (byPos ? 4 : 2) * (4 * kRyxPadK + 2 * ((maxSpan + 3) & ~3));
+    const int ldsBytes = (byPos ? 2 * std::max(2, d.posRows) : 2) * (4 * kRyxPadK + 2 * ((maxSpan + 3) & ~3));
     const int rows = rowEnd - rowBegin;
     // bands: ~6 rounds of resident workgroups, >= 32 rows each (steady clock, x256: 1080p -> 1366x768
     // 12 bands 0.306 ms vs 5 bands 0.315, 1080p -> 1024x576 equal; profiles/r05/steady_ryg_bands.txt)

@@ -1709,27 +1709,38 @@ bool build_ryu_positions(int dstH, RyxTables *t)
 {
     t->posRec.clear();
     t->posBase = 0;
+    t->posRows = 0;
     if (!t->ok || !t->general || t->rowLoads != 1 || dstH < 1 || t->rowRec.size() < static_cast<size_t>(2 * dstH))
         return false;
     std::vector<int32_t> pos;
     const int32_t s0 = t->rowRec[0];
+    int most = 0;
     for (int y = 0; y < dstH; ++y) {
         const int32_t s = t->rowRec[static_cast<size_t>(2 * y)], c = t->rowRec[static_cast<size_t>(2 * y + 1)];
-        const int64_t k = static_cast<int64_t>(s) - s0, n = static_cast<int64_t>(pos.size() / 4);
+        const int64_t k = static_cast<int64_t>(s) - s0, n = static_cast<int64_t>(pos.size() / kRyuRec);
         if (k == n) {
-            pos.insert(pos.end(), {y, 1, c, c});
-        } else if (k == n - 1 && pos[pos.size() - 3] == 1) {
-            pos[pos.size() - 3] = 2;
-            pos[pos.size() - 1] = c;
+            pos.insert(pos.end(), kRyuRec, c);  // (tap offsets past the position's rows: its last row's)
+            pos[pos.size() - kRyuRec] = y;
+            pos[pos.size() - kRyuRec + 1] = 1;
+        } else if (k == n - 1 && pos[pos.size() - kRyuRec + 1] < kRyuRec - 2) {
+            const int j = ++pos[pos.size() - kRyuRec + 1];
+            for (int q = j + 1; q < kRyuRec; ++q)
+                pos[pos.size() - kRyuRec + q] = c;
         } else {
-            return false;  // a position of 3 rows, or a window that moved back or skipped a row
+            return false;  // a window that moved back or skipped a row, or too many rows
         }
+        most = std::max(most, pos[pos.size() - kRyuRec + 1]);
     }
-    const int32_t lastC = pos.back();
+    if (most > kRyuMaxRows)
+        return false;
+    std::vector<int32_t> last(pos.end() - kRyuRec, pos.end());
+    last[0] = dstH;
+    last[1] = 1;
     for (int k = 0; k < kRyuPosPad; ++k)
-        pos.insert(pos.end(), {dstH, 1, lastC, lastC});
+        pos.insert(pos.end(), last.begin(), last.end());
     t->posRec = std::move(pos);
     t->posBase = s0;
+    t->posRows = std::max(2, most);
     return true;
 }
 

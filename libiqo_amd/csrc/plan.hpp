@@ -272,10 +272,12 @@ struct RyxTables {
     int rowLoads = 2;                      // general rows: 2 (downscale), 1 (upscale) new rows per output row
     std::vector<int32_t> rowRec;           // dstH x 2
     // general upscale rows walked by window position (build_ryu_positions, kernels.hip ryu_kernel):
-    // record s - posBase = {first output row whose window starts at s, rows (1 or 2), tap offsets of
-    // that row and the next}, 4 ints each, kRyuPosPad padding records; empty: no such walk
+    // record s - posBase = {first output row whose window starts at s, rows (1 .. kRyuMaxRows), tap
+    // offsets of those rows (then repeats)}, kRyuRec ints each, kRyuPosPad padding records; empty:
+    // no such walk
     std::vector<int32_t> posRec;
     int posBase = 0;
+    int posRows = 0;  // the most rows any position holds (at least 2)
     // run mode of the upscale walk (build_ryu_runs): groups of 4 adjacent output columns (x = 4g ..
     // 4g + 3) read one run of runPairs work-row dwords from the group's lowest even start; column x's
     // coefficient pairs at their offset in a zero-padded run: dstW x runPairs; empty: per-column mode
@@ -292,9 +294,11 @@ void build_ryx(const Plan &p, RyxTables *t);
 void build_ryg(const Plan &p, RyxTables *t);
 // Window-position records of a general upscale (build_ryg with rowLoads 1), in t->posRec / posBase.
 // At an upscale the reference's srcOY advances by 0 or 1 per output row, so every window position
-// between the first and the last holds at least one row; the kernel takes positions of 1 or 2 rows
-// (rows that grow by at most 2).  Returns false (and leaves posRec empty) otherwise.
+// between the first and the last holds at least one row; the kernel takes positions of up to
+// kRyuMaxRows rows (rows that grow by at most 3).  Returns false (and leaves posRec empty) otherwise.
 constexpr int kRyuPosPad = 8;  // records past the last position (ryu_kernel reads a band's last + 2)
+constexpr int kRyuRec = 8;     // ints per position record: {first row, rows, tap offsets of 6 rows}
+constexpr int kRyuMaxRows = 3; // rows per position the kernel instantiates (rows that grow by <= 3)
 bool build_ryu_positions(int dstH, RyxTables *t);
 // The run-mode column table (colRun / runPairs) for groups of 4 adjacent columns whose windows fit in
 // NP + 1 or NP + 2 dwords from the group's first even start (upscaled columns); false otherwise.

@@ -25,7 +25,10 @@ BENCH = {"c2": ("lanczos_stream", 1024), "c3": ("area_int", 64), "c4": ("linear_
          "g1": ("lanczos_d32", 128), "g2": ("lanczos_up2", 32), "g3": ("area_d32", 128),
          "g4": ("lanczos_d31", 128), "g5": ("ryx", 256), "g6": ("area_int", 128),
          "h1": ("area_int", 128, "linear_d2_kernel"), "h2": ("ryx", 128), "h3": ("lanczos_stream", 128), "h4": ("lanczos_up2", 64),
-         "h5": ("linear_up2", 64), "h6": ("ryx", 128)}
+         "h5": ("linear_up2", 64), "h6": ("ryx", 128),
+         # round 6: the general-row kernels (upscale rows on ryu_kernel, 3..4:1 downscale rows on ryg_kernel)
+         "u1": ("ryx", 256), "u2": ("ryg", 256, "ryu_kernel"), "u3": ("ryg", 256, "ryu_kernel"),
+         "w6": ("ryg", 128, "ryg_kernel")}
 
 
 def per_dispatch(dirname, counter, kname):

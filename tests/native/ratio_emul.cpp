@@ -350,7 +350,7 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
             return 1;
         const bool lz = method == 0;
         const int TK = r.taps, NP = r.NP;
-        const size_t nPosRec = r.posRec.size() / 4;
+        const size_t nPosRec = r.posRec.size() / kRyuRec;
         std::vector<uint16_t> wrow(static_cast<size_t>(srcW + 2 * kRyxPad), 0);
         std::vector<uint8_t> first;
         for (const int rpb : {dstH, 7, 13, 1, 64}) {
@@ -363,12 +363,12 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
                     const size_t ri = static_cast<size_t>(pA - r.posBase + q);
                     if (ri + 2 >= nPosRec)
                         return -2;  // the kernel's look-ahead would read past the table
-                    const int32_t *rc = &r.posRec.at(4 * ri);
+                    const int32_t *rc = &r.posRec.at(kRyuRec * ri);
                     const int ya = std::max(rc[0], y0), cnt = std::min(rc[0] + rc[1], y1) - ya;
-                    if (cnt < 1 || cnt > 2 || (cnt == 2 && ya != rc[0]))
+                    if (cnt < 1 || cnt > r.posRows || (q > 0 && ya != rc[0]))
                         return -4;
                     for (int k = 0; k < cnt; ++k) {
-                        const int y = ya + k, co = k ? rc[3] : (ya == rc[0] ? rc[2] : rc[3]);
+                        const int y = ya + k, co = rc[2 + (ya - rc[0]) + k];
                         ++written.at(static_cast<size_t>(y));
                         for (int c = 0; c < srcW; ++c) {
                             uint16_t acc = 0;

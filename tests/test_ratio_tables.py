@@ -105,7 +105,10 @@ def _shapes():
            ("ryu", "lanczos", 2, 64, 9, 96, 17),
            ("ryu_run", "lanczos", 3, 1024, 576, 1920, 1080), ("ryu_run", "lanczos", 3, 1366, 768, 1920, 1080),
            ("ryu_run", "lanczos", 4, 1024, 576, 1920, 1080), ("ryu_run", "lanczos", 2, 100, 37, 130, 71),
-           ("ryu_run", "lanczos", 3, 1367, 769, 1921, 1081)]
+           ("ryu_run", "lanczos", 3, 1367, 769, 1921, 1081),
+           # rows that grow by 2 .. 3 (round 6: up to 3 rows per window position)
+           ("ryu", "lanczos", 3, 640, 480, 1920, 1080), ("ryu_run", "lanczos", 3, 640, 480, 1920, 1080),
+           ("ryu_run", "lanczos", 2, 854, 400, 1920, 1080), ("ryu", "lanczos", 3, 100, 30, 250, 88)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -133,7 +136,7 @@ def _shapes():
         out.append(("ryu", "lanczos", rng.choice((2, 3, 4)), sw, uh, rng.randint(sw, min(4096, 2 * sw)),
                     rng.randint(uh + 1, 2 * uh)))
         out.append(("ryu_run", "lanczos", rng.choice((2, 3, 4)), sw, uh, rng.randint(sw + 1, min(4096, 2 * sw)),
-                    rng.randint(uh + 1, 2 * uh)))
+                    rng.randint(uh + 1, 3 * uh)))
         uw = sw // 2 & ~3  # 4:9 rows, columns upscaled (<= 4 coefficient pairs)
         out.append(("ryx", "lanczos", rng.choice((2, 3)), uw, 4 * b + 16, rng.randint(uw, min(4096, 3 * uw)), 9 * b + 36))
     return out
