@@ -2356,6 +2356,11 @@ __device__ __forceinline__ void linear_up2_kernel_body(const LinearArgs &a, cons
 template <int PD, bool NTST, int F>
 __global__ __launch_bounds__(256) void linear_up2_kernel(LinearArgs a)
 {
+    // (plain block order, neighbouring bands on different XCDs.  Round 6: an XCD-aware order
+    // (xcd_spread, each XCD a contiguous run of (frame, band) blocks) removes the re-read of the
+    // source row two bands share -- HBM traffic 1.117x -> 1.0002x algorithmic -- but is 9 % slower
+    // (C4 x256 0.508 vs 0.464 ms, profiles/r06/c4_xcd_order.txt): every XCD streaming its own
+    // address range spreads the requests over fewer channels at a time)
     linear_up2_kernel_body<PD, NTST, F>(a, blockIdx.x, blockIdx.y);
 }
 

@@ -2604,7 +2604,11 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     if (bands <= 0) {
         const int64_t resident = std::max(1, resident_waves(kern, threads, ldsBytes) / (threads / 64));
         const int64_t perBand = static_cast<int64_t>(io.frames) * d.parts;
-        bands = static_cast<int>(std::min<int64_t>((6 * resident + perBand - 1) / perBand, std::max(1, rows / 32)));
+        // (round 6: ~3 rounds at 4 rows per output row, whose 22-24-row windows make a band's halo
+        // costly -- 4K -> 1024x576 x128: 6 bands 0.485 ms, 12 bands 0.494, 18 0.506,
+        // profiles/r06/c4_xcd_order.txt)
+        const int rounds = d.nl >= 4 ? 3 : 6;
+        bands = static_cast<int>(std::min<int64_t>((rounds * resident + perBand - 1) / perBand, std::max(1, rows / 32)));
     }
     bands = std::max(1, std::min(bands, rows));
     const int rpb = (rows + bands - 1) / bands;
