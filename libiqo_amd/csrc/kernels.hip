@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void tile_kernel(TileArgs a)
     // (round 2: column tiles fastest and plain dispatch order both slower, profiles/r02/tile_xcd_ab.txt).
     int tileX, tileY, frame;
     {
-        const unsigned lg = xcd_spread(blockIdx.x, a.nTiles);
+        const unsigned lg = xcd_chunks(blockIdx.x, a.nTx * a.nTy, a.nTiles);
         const unsigned rest = lg / static_cast<unsigned>(a.nTy);
         tileY = static_cast<int>(lg - rest * static_cast<unsigned>(a.nTy));
         frame = static_cast<int>(rest / static_cast<unsigned>(a.nTx));
@@ -1389,12 +1389,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 12 ? 2
         // XCD's CUs finish together; neighbouring bands of a frame share that XCD's L2 (halo rows)
         const int x = static_cast<int>(blockIdx.x & 7u), idx = static_cast<int>(blockIdx.x >> 3);
         const int F8 = a.framesPerXcd, nLong = (F8 - 1) * a.bands;
+        // XCD x takes frames x, x + 8, ... (round 6): the 8 XCDs work on 8 neighbouring frames at a
+        // time instead of 8 regions F8 frames apart (C2 x256 0.479 -> 0.467 ms; variant builds,
+        // debug flag 128: the old contiguous ranges)
+        const bool inter = !(IQO_DBG(a) & 128);  // (round 6 default: interleaved, profiles/r06/xcd_chunks.txt)
         if (idx < nLong) {
             const int q = idx / a.bands;
-            by = static_cast<unsigned>(x * F8 + q);
+            by = static_cast<unsigned>(inter ? 8 * q + x : x * F8 + q);
             bx = static_cast<unsigned>(idx - q * a.bands);
         } else {
-            by = static_cast<unsigned>(x * F8 + F8 - 1);
+            by = static_cast<unsigned>(inter ? 8 * (F8 - 1) + x : x * F8 + F8 - 1);
             bx = static_cast<unsigned>(idx - nLong);
             rpb = a.tailRows;
             if (static_cast<int>(bx) >= a.tailBands)
@@ -1405,7 +1409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 12 ? 2
         // halo rows two neighbouring bands share hit that XCD's L2, and each XCD streams from
         // 1/8 of the batch's address range
         const unsigned bands = gridDim.x;
-        const unsigned lg = xcd_spread(by * bands + bx, bands * gridDim.y);
+        const unsigned lg = xcd_chunks(by * bands + bx, bands, bands * gridDim.y);
         by = lg / bands;
         bx = lg - by * bands;
     }
@@ -1739,7 +1743,7 @@ __global__ __launch_bounds__(256) void walk_kernel(WalkArgs a)
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     // flat wave id -> (strip, band, frame); XCD-spread by workgroup, so neighbouring strips and
     // bands (which share halo rows and columns) run on one XCD's L2
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.strips * a.bands + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;  // whole wave; the kernel has no barrier
     const int strip = a.stripLo + static_cast<int>(gw % static_cast<unsigned>(a.strips)) * a.stripStride;

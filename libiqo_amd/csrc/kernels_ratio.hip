@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void lanczos_up2_kernel(Up2Args a)
     __shared__ __attribute__((aligned(16))) uint8_t stage[F == 3 ? 4 * 2048 : 16];  // 3x: store_row24
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.bands * a.wavesPerRow + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;  // whole wave; no barrier in this kernel
     const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void lanczos_d32_kernel(D32Args a)
     __shared__ int4 park[4][2][8][2];  // per wave, side, row slot: the edge lane's 8 raw sums
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.bands * a.wavesPerRow + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;  // whole wave; no barrier in this kernel
     const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256) void lanczos_d31_kernel(D31Args a)
     __shared__ int4 park[4][2][8];  // per wave, side, row slot: the edge lane's 4 raw sums
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.bands * a.wavesPerRow + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;  // whole wave; no barrier in this kernel
     const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 20 && !
     const RyxDev &d = a.d;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int t = static_cast<int>(threadIdx.x);
-    const unsigned blk0 = xcd_spread(blockIdx.x, gridDim.x);
+    const unsigned blk0 = xcd_chunks(blockIdx.x, a.bands * d.parts, gridDim.x);
     if (blk0 >= a.nBlocks)
         return;  // whole workgroup
     // column part (d.parts workgroups per row), then band, then frame
@@ -1242,6 +1242,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 22 ? 2 
     const RygDev &d = a.d;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int t = static_cast<int>(threadIdx.x);
+    // (xcd_spread here: the chunk map of the other kernels was 3.8 % slower on 1080p -> 1366x768,
+    // profiles/r06/xcd_chunks.txt)
     const unsigned blk0 = xcd_spread(blockIdx.x, gridDim.x);
     if (blk0 >= a.nBlocks)
         return;  // whole workgroup
@@ -1512,7 +1514,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void r
     const RygDev &d = a.d;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int t = static_cast<int>(threadIdx.x);
-    const unsigned blk0 = xcd_spread(blockIdx.x, gridDim.x);
+    const unsigned blk0 = xcd_chunks(blockIdx.x, a.bands * d.parts, gridDim.x);
     if (blk0 >= a.nBlocks)
         return;  // whole workgroup
     const int part = static_cast<int>(blk0 % static_cast<unsigned>(d.parts));
@@ -1795,7 +1797,7 @@ __global__ __launch_bounds__(256) void lanczos_u23_kernel(U23Args a)
     __shared__ int4 park[4][2][3 * U][3];  // per wave, side, row slot: the edge lane's 12 raw sums
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.bands * a.wavesPerRow + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;
     const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
@@ -2012,7 +2014,7 @@ __global__ __launch_bounds__(256) void linear_u23_kernel(L23Args a)
     const L23Dev &d = a.d;
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.bands * a.wavesPerRow + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;
     const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
@@ -2154,7 +2156,7 @@ __global__ __launch_bounds__(256) void area_d32_kernel(A32Args a)
     const A32Dev &d = a.d;
     const int lane = static_cast<int>(threadIdx.x) & 63;
     const int wib = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
-    const unsigned gw = xcd_spread(blockIdx.x, gridDim.x) * 4u + static_cast<unsigned>(wib);
+    const unsigned gw = xcd_chunks(blockIdx.x, (a.bands * a.wavesPerRow + 3) / 4, gridDim.x) * 4u + static_cast<unsigned>(wib);
     if (gw >= a.nWaves)
         return;
     const int wcol = static_cast<int>(gw % static_cast<unsigned>(a.wavesPerRow));
