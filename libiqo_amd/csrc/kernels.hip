@@ -1409,6 +1409,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NY > 12 ? 2
         // halo rows two neighbouring bands share hit that XCD's L2, and each XCD streams from
         // 1/8 of the batch's address range
         const unsigned bands = gridDim.x;
+        // (chunks of one frame's bands: 9 .. 45 bands or 2 frames per chunk measured the same or
+        // slower, profiles/r06/xcd_chunks.txt)
         const unsigned lg = xcd_chunks(by * bands + bx, bands, bands * gridDim.y);
         by = lg / bands;
         bx = lg - by * bands;

@@ -19,12 +19,15 @@ def main():
     ap.add_argument("line")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--kernel", default="", help="substring of the kernel to summarise (default: the one taking most time)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     tot = collections.Counter()
     for r in rows:
         tot[r["Kernel_Name"]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     top = tot.most_common(1)[0][0]
+    if a.kernel:  # (the default bench also launches the C3 / C4 secondary lines and probes)
+        top = max((k for k in tot if a.kernel in k), key=lambda k: tot[k])
     groups = collections.OrderedDict()
     for r in sorted(rows, key=lambda r: int(r["Start_Timestamp"])):
         if r["Kernel_Name"] != top:
