@@ -110,10 +110,10 @@ int iqo_hip_plan_prepare(iqo_hip_plan *plan);
  * only, never the output bytes.  IQO_HIP_EINVAL for an unknown key or value.
  * With IQO_HIP_TUNING=1 in the environment the call also takes the A/B keys of
  * libiqo_amd/csrc/abi.hip (kernel family switches "tile", "walk", "up2", "d32", "a32", "u23",
- * "l23", "d31", "ryx", "ryg"; schedules "tile_rows", "stack", "rounds", "tail", "prefetch",
- * "ratio_prefetch", "ryx_split", "ryx_adj", "ryx_cpt", "ryx_uc", "ryg_cpt", "stream_variant",
- * "lanes", "chunk_frames"), which the tests and tuning scripts use; they are not part of the
- * supported interface. */
+ * "l23", "d31", "ryx", "ryg", "ryu"; schedules "tile_rows", "stack", "rounds", "tail", "prefetch",
+ * "ratio_prefetch", "ryx_split", "ryx_adj", "ryx_cpt", "ryx_uc", "ryg_cpt", "ryu_run",
+ * "stream_variant", "lanes", "chunk_frames"), which the tests and tuning scripts use; they are not
+ * part of the supported interface. */
 int iqo_hip_plan_set_option(iqo_hip_plan *plan, const char *key, long value);
 
 /* Drop-in resize with HOST pointers (byte strides), synchronous: H2D, kernels, D2H. */
