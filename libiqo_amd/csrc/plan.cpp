@@ -1710,19 +1710,26 @@ bool build_ryu_positions(int dstH, RyxTables *t)
     t->posRec.clear();
     t->posBase = 0;
     t->posRows = 0;
-    if (!t->ok || !t->general || t->rowLoads != 1 || dstH < 1 || t->rowRec.size() < static_cast<size_t>(2 * dstH))
+    if (!t->ok || !t->general || dstH < 1 || t->rowRec.size() < static_cast<size_t>(2 * dstH))
         return false;
     std::vector<int32_t> pos;
     const int32_t s0 = t->rowRec[0];
     int most = 0;
     for (int y = 0; y < dstH; ++y) {
         const int32_t s = t->rowRec[static_cast<size_t>(2 * y)], c = t->rowRec[static_cast<size_t>(2 * y + 1)];
-        const int64_t k = static_cast<int64_t>(s) - s0, n = static_cast<int64_t>(pos.size() / kRyuRec);
+        const int64_t k = static_cast<int64_t>(s) - s0;
+        // (downscales: the positions a window skips hold no rows)
+        while (static_cast<int64_t>(pos.size() / kRyuRec) < k) {
+            pos.insert(pos.end(), kRyuRec, c);
+            pos[pos.size() - kRyuRec] = y;
+            pos[pos.size() - kRyuRec + 1] = 0;
+        }
+        const int64_t n = static_cast<int64_t>(pos.size() / kRyuRec);
         if (k == n) {
             pos.insert(pos.end(), kRyuRec, c);  // (tap offsets past the position's rows: its last row's)
             pos[pos.size() - kRyuRec] = y;
             pos[pos.size() - kRyuRec + 1] = 1;
-        } else if (k == n - 1 && pos[pos.size() - kRyuRec + 1] < kRyuRec - 2) {
+        } else if (k == n - 1 && pos[pos.size() - kRyuRec + 1] >= 1 && pos[pos.size() - kRyuRec + 1] < kRyuRec - 2) {
             const int j = ++pos[pos.size() - kRyuRec + 1];
             for (int q = j + 1; q < kRyuRec; ++q)
                 pos[pos.size() - kRyuRec + q] = c;
@@ -1740,7 +1747,7 @@ bool build_ryu_positions(int dstH, RyxTables *t)
         pos.insert(pos.end(), last.begin(), last.end());
     t->posRec = std::move(pos);
     t->posBase = s0;
-    t->posRows = std::max(2, most);
+    t->posRows = most;
     return true;
 }
 

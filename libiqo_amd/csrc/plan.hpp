@@ -277,7 +277,7 @@ struct RyxTables {
     // no such walk
     std::vector<int32_t> posRec;
     int posBase = 0;
-    int posRows = 0;  // the most rows any position holds (at least 2)
+    int posRows = 0;  // the most rows any position holds (downscales: 1, positions between rows hold 0)
     // run mode of the upscale walk (build_ryu_runs): groups of 4 adjacent output columns (x = 4g ..
     // 4g + 3) read one run of runPairs work-row dwords from the group's lowest even start; column x's
     // coefficient pairs at their offset in a zero-padded run: dstW x runPairs; empty: per-column mode

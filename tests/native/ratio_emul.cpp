@@ -335,7 +335,7 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
         return touch == -1 ? -3 : 0;  // (keeps the look-ahead reads)
     }
     if (kind == 10 || kind == 11) {
-        // ryu_kernel (general upscale rows walked by window position, plan.cpp build_ryu_positions):
+        // ryu_kernel / ryp_kernel (general rows walked by window position, plan.cpp build_ryu_positions):
         // for each band [y0, y1) the kernel takes positions pA = s(y0) .. s(y1 - 1); position p's
         // record gives the output rows whose window starts at pA + p, clipped to the band, and their
         // tap offsets; it reads the records of positions p + 1 and p + 2 unclamped.  Emulated over
@@ -365,6 +365,8 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
                         return -2;  // the kernel's look-ahead would read past the table
                     const int32_t *rc = &r.posRec.at(kRyuRec * ri);
                     const int ya = std::max(rc[0], y0), cnt = std::min(rc[0] + rc[1], y1) - ya;
+                    if (cnt <= 0 && (rc[1] == 0 || rc[0] + rc[1] <= y0))
+                        continue;  // a position without rows (downscales) or whose rows precede the band
                     if (cnt < 1 || cnt > r.posRows || (q > 0 && ya != rc[0]))
                         return -4;
                     for (int k = 0; k < cnt; ++k) {
@@ -388,15 +390,25 @@ int ratio_emul(int kind, int method, unsigned degree, int srcW, int srcH, int ds
                                 for (int k = x & ~3; k < std::min(dstW, (x & ~3) + 4); ++k)
                                     a = std::min(a, r.cols.at(static_cast<size_t>(k) * 4) / 2);
                             const int nq = run ? r.runPairs : NP;
-                            int64_t sum = 1 << 19;
+                            int64_t sum = lz ? (1 << 19) : (1 << 22);
                             for (int q2 = 0; q2 < nq; ++q2) {
                                 const uint32_t c = run ? r.colRun.at(static_cast<size_t>(x) * nq + q2)
                                                        : r.colCoef.at(static_cast<size_t>(x) * NP + q2);
                                 const uint16_t w0 = wrow.at(static_cast<size_t>(a + 2 * q2)), w1 = wrow.at(static_cast<size_t>(a + 2 * q2 + 1));
-                                sum += static_cast<int16_t>(w0) * static_cast<int16_t>(c & 0xffffu) +
-                                       static_cast<int16_t>(w1) * static_cast<int16_t>(c >> 16);
+                                if (lz)
+                                    sum += static_cast<int16_t>(w0) * static_cast<int16_t>(c & 0xffffu) +
+                                           static_cast<int16_t>(w1) * static_cast<int16_t>(c >> 16);
+                                else
+                                    sum += static_cast<int64_t>(w0) * (c & 0xffffu) + static_cast<int64_t>(w1) * (c >> 16);
                             }
-                            dst[static_cast<size_t>(y) * dstW + x] = edge_div(static_cast<int>(sum), static_cast<uint32_t>(cx[1]), cx[2]);
+                            uint8_t o;
+                            if (lz) {
+                                o = edge_div(static_cast<int>(sum), static_cast<uint32_t>(cx[1]), cx[2]);
+                            } else {  // (Area / Linear: ryg_kernel's u16 sums, (s + 2^22) >> 23)
+                                const uint16_t u = static_cast<uint16_t>(static_cast<int16_t>(static_cast<int>(static_cast<uint32_t>(sum)) >> 23));
+                                o = static_cast<uint8_t>(u > 255 ? 255 : u);
+                            }
+                            dst[static_cast<size_t>(y) * dstW + x] = o;
                         }
                     }
                 }

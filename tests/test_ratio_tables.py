@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 METHODS = {"lanczos": 0, "area": 1, "linear": 2}
 KINDS = {"lanczos_d32": 0, "lanczos_up2": 1, "area_d32": 2, "lanczos_u23": 3, "linear_u23": 4, "lanczos_d31": 5, "ryx": 6, "linear_up": 8,
-         "linear_d2": 7, "ryg": 9, "ryu": 10, "ryu_run": 11}
+         "linear_d2": 7, "ryg": 9, "ryu": 10, "ryu_run": 11, "ryp": 10}
 
 
 @pytest.fixture(scope="module")
@@ -108,7 +108,13 @@ def _shapes():
            ("ryu_run", "lanczos", 3, 1367, 769, 1921, 1081),
            # rows that grow by 2 .. 3 (round 6: up to 3 rows per window position)
            ("ryu", "lanczos", 3, 640, 480, 1920, 1080), ("ryu_run", "lanczos", 3, 640, 480, 1920, 1080),
-           ("ryu_run", "lanczos", 2, 854, 400, 1920, 1080), ("ryu", "lanczos", 3, 100, 30, 250, 88)]
+           ("ryu_run", "lanczos", 2, 854, 400, 1920, 1080), ("ryu", "lanczos", 3, 100, 30, 250, 88),
+           # downscale rows walked by window position (ryp, round 6): 1..2:1, 2..3:1, 3..4:1, Area, Linear
+           ("ryp", "lanczos", 3, 1920, 1080, 1366, 768), ("ryp", "lanczos", 2, 1920, 1080, 1024, 576),
+           ("ryp", "lanczos", 3, 3840, 2160, 1366, 768), ("ryp", "lanczos", 3, 3840, 2160, 1024, 576),
+           ("ryp", "area", 0, 1920, 1080, 1366, 768), ("ryp", "area", 0, 3840, 2160, 1024, 576),
+           ("ryp", "linear", 0, 1920, 1080, 1366, 768), ("ryp", "lanczos", 4, 1918, 1078, 1366, 768),
+           ("ryp", "lanczos", 3, 301, 170, 100, 45)]
     for _ in range(6):
         a, b = rng.randint(2, 40), rng.randint(4, 60)
         out.append(("lanczos_d32", "lanczos", 3, 12 * a, 3 * b, 8 * a, 2 * b))
@@ -132,6 +138,9 @@ def _shapes():
         gh = 8 * rng.randint(8, 40)
         out.append(("ryg", rng.choice(("lanczos", "area")) if hr > 1 else "lanczos", rng.choice((2, 3)), sw, gh,
                     max(16, int(sw / hr) & ~1), max(8, int(gh / hr))))
+        dh_ = rng.randint(40, 300)  # downscale rows by 1 .. 4 (ryp)
+        out.append(("ryp", rng.choice(("lanczos", "area")), rng.choice((2, 3)), sw, int(dh_ * rng.uniform(1.05, 3.4)),
+                    max(16, int(sw / rng.uniform(1.05, 2.0)) & ~1), dh_))
         uh = rng.randint(8, 200)  # upscale rows by 1 .. 2 (ryu)
         out.append(("ryu", "lanczos", rng.choice((2, 3, 4)), sw, uh, rng.randint(sw, min(4096, 2 * sw)),
                     rng.randint(uh + 1, 2 * uh)))
