@@ -614,6 +614,9 @@ def main():
         mine, host_win, wins, bands_out, rot = band_buffers(r, frames, sw, dw, dh, rank, world, dev, args.band_src,
                                                             args.rotate)
         mine = mine._replace(device=gpu)
+        # every rank's shard (rows and windows; only their indices and rank 0's own device matter to
+        # the gather, which moves the other bands by IPC handle)
+        shards = [mine if s.index == rank else s for s in shard.make_shards(r, dh, list(range(world)))]
         t_sc = 0.0
         be = shard.HipBandBackend(lambda device: r if device == mine.device else make(device),
                                   host_win if host_win is not None else wins[0], -1 if host_win is not None else gpu,
