@@ -2277,8 +2277,10 @@ hipError_t launch_up2(const Up2Dev &u, const Io &io, int rowBegin, int rowEnd, i
     // bands: one trip (NT source steps, F NT output rows) each -- the most waves with no partial
     // trip (fresh batches, 2x 1080p 125 frames: 12-row bands 54.9 % of 8 TB/s vs 53.2 % at ~2.5
     // rounds of resident waves; 3x 720p 141 frames: 18-row bands 47.4 % vs 39.3 %)
+    // (round 6, steady clock: bands of at most 12 rows -- 3x Lanczos-3 720p -> 4K x64: 180 bands of
+    // 12 rows 0.149 ms vs 120 of 18 rows 0.164, profiles/r06/band_sweeps.txt)
     if (bands <= 0)
-        bands = std::max(1, rows / (u.F * u.NT));
+        bands = std::max(1, rows / std::min(u.F * u.NT, 12));
     bands = std::max(1, std::min(bands, rows));
     int rpb = (rows + bands - 1) / bands;
     rpb = (rpb + u.F - 1) / u.F * u.F;  // a band's steps produce whole groups of F rows
@@ -2326,11 +2328,10 @@ hipError_t launch_d32(const D32Dev &d, const Io &io, int rowBegin, int rowEnd, i
     const int evenBegin = rowBegin & ~1;
     const int rows = rowEnd - evenBegin;
     // bands: ~2.5 rounds of resident waves, whole trips (8 rows) per band, >= 16 rows
-    if (bands <= 0) {
-        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
-        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
-        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
-    }
+    // (round 6, steady clock: bands of ~16 rows whatever the batch -- 1080p -> 720p x128: 45 bands
+    // 0.0827 ms vs the ~2.5-rounds choice 0.0877, profiles/r06/band_sweeps.txt)
+    if (bands <= 0)
+        bands = std::max(1, rows / 16);
     const int trip = d.variant == 0 ? 8 : 6;  // output rows per unrolled trip (2 U)
     bands = std::max(1, std::min(bands, (rows + trip - 1) / trip));
     int rpb = (rows + bands - 1) / bands;
@@ -2373,12 +2374,10 @@ hipError_t launch_d31(const D31Dev &d, const Io &io, int rowBegin, int rowEnd, i
         return hipErrorInvalidValue;
     const int rows = rowEnd - rowBegin;
     const int trip = d.variant == 0 ? 5 : 4;  // output rows per unrolled trip (U)
-    // bands: ~2.5 rounds of resident waves, whole trips per band, >= 16 rows
-    if (bands <= 0) {
-        const int64_t resident = std::max(1, resident_waves(kern, 256, 0));
-        const int64_t perBand = static_cast<int64_t>(wpr) * io.frames;
-        bands = static_cast<int>(std::min<int64_t>((5 * resident / 2 + perBand - 1) / perBand, std::max(1, rows / 16)));
-    }
+    // bands of two trips (round 6, steady clock: 4K -> 720p x128: 72 bands of 10 rows 0.235 ms vs
+    // the ~2.5-rounds choice 0.261, profiles/r06/band_sweeps.txt)
+    if (bands <= 0)
+        bands = std::max(1, rows / (2 * trip));
     bands = std::max(1, std::min(bands, (rows + trip - 1) / trip));
     int rpb = (rows + bands - 1) / bands;
     rpb = (rpb + trip - 1) / trip * trip;
