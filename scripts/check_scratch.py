@@ -6,9 +6,9 @@ the compiler move the whole register window to scratch; this makes such regressi
 import re
 import sys
 
-ASM = sys.argv[1] if len(sys.argv) > 1 else "libiqo_amd/build/kernels-hip-amdgcn-amd-amdhsa-gfx950.s"
+ASMS = sys.argv[1:] or ["libiqo_amd/build/%s-hip-amdgcn-amd-amdhsa-gfx950.s" % k for k in ("kernels", "kernels_ratio")]
 cur, counts = None, {}
-for line in open(ASM):
+for line in (ln for f in ASMS for ln in open(f)):
     m = re.match(r"^(_Z\S+):", line)
     if m:
         cur = m.group(1)

@@ -11,9 +11,9 @@ timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_dr
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_driver_cmd -o run -- python3 $ROOT/bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-probe > $OUT/trace_driver_cmd.json 2> $OUT/trace_driver_cmd.err || { tail -20 $OUT/trace_driver_cmd.err; exit 1; }
 cd $ROOT
-python3 scripts/trace_summary.py $(ls $OUT/trace_driver_cmd/*kernel_trace.csv | head -1) $OUT/trace_driver_cmd.json --steps 20 --warmup 5 > $OUT/trace_summary.txt 2>&1 || true
-PMC_CFGS="c2" bash scripts/gpu_ci.sh pmc > $OUT/pmc.txt 2>&1 || { tail -20 $OUT/pmc.txt; exit 1; }
-python3 scripts/pmc_to_json.py gpurun_out c2 --round r06 > $OUT/pmc_c2_line.txt && cp profiles/pmc_c2.json $OUT/pmc_c2.json
+python3 scripts/trace_summary.py $(ls $OUT/trace_driver_cmd/*kernel_trace.csv | head -1) $OUT/trace_driver_cmd.json --steps 20 --warmup 5 --kernel lanczos_symb > $OUT/trace_summary.txt 2>&1 || true
+PMC_CFGS="c2 w6" bash scripts/gpu_ci.sh pmc > $OUT/pmc.txt 2>&1 || { tail -20 $OUT/pmc.txt; exit 1; }
+python3 scripts/pmc_to_json.py gpurun_out c2 --round r06 > $OUT/pmc_c2_line.txt && cp profiles/pmc_c2.json $OUT/pmc_c2.json && python3 scripts/pmc_to_json.py gpurun_out w6 --round r06 >> $OUT/pmc_c2_line.txt && cp profiles/pmc_w6.json $OUT/pmc_w6.json
 timeout -k 10 400 python bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err || { tail -20 $OUT/bench_default.err; exit 1; }
 python3 - <<'PY'
 import json
