@@ -60,7 +60,7 @@ struct iqo_hip_plan {
     int stack = 1;          // block-shared streamer: narrow frames side by side in one workgroup (speed only)
     int ryxAdj = 1;         // ratio-Y kernel: adjacent column pairs per thread where they fit (speed only)
     int ryxCpt = 1;         // ratio-Y kernel: 4 output columns per thread at the Lanczos 4:9 upscales (speed only)
-    int ryxSplit = 1;       // ratio-Y kernel: 0 one workgroup per row, 1 two, 2 four (speed only)
+    int ryxSplit = 1;       // ratio-Y kernel column parts (speed only; option ryx_split)
     int rygCpt = 0;         // general-row kernel on rows of > 1024 outputs: output columns per thread (0 = auto)
     int ryxUc = 1;          // ratio-Y kernel: uniform column coefficients as scalars where every column has the same
     int lanes = 0;          // symmetric streamer producing lanes per wave (0 = auto)
@@ -1086,8 +1086,26 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
         d.cpt = h->rygCpt ? h->rygCpt : std::min(cap, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
         if (t.rowLoads >= 3)
             d.cpt = 2;  // (downscales past 2:1: 2 columns per thread is the only instantiation)
-        const int tw = h->ryxSplit == 2 ? 128 : 64;
-        if ((h->ryxSplit >= 2 && split_min(tw)) || (h->ryxSplit == 1 && split(2, 256)) || split(1, 512))
+        // (round 6, late) parts of ONE wave where the row fits 16 of them: a barrier over one wave
+        // instead of 4 or 8, and no 512-thread part half idle (2560 columns took two parts of 512
+        // threads for 640 columns' work).  Lanczos downscale rows: 2560x1440 -> 1024x576 0.554 ->
+        // 0.339 ms, -> 1920x1080 0.393 -> 0.255, 4K -> 1600x900 0.429 -> 0.363, 1080p -> 1366x768
+        // -2.6 %; rows that need more than 16 parts of one wave take parts of two waves below 4 rows
+        // per output row (4K -> 1366x768 0.399 -> 0.332; at 4 rows the 22-tap kernel, which spills,
+        // was 11 % slower in them).  Upscale rows keep one or two workgroups where those hold the
+        // row (1024x576 -> 1080p was 6 % slower in one-wave parts) and take one-wave parts where
+        // not (1366x768 -> 2560x1440 0.263 -> 0.225).  Area rows keep the 8-wave parts (4K ->
+        // 1366x768 12 % slower in one-wave parts).  profiles/r06/ryg_split.txt; option ryx_split = 4
+        // restores the previous rule.
+        if (h->ryxSplit == 1 && d.lanczos) {
+            if (t.rowLoads >= 2 && (split_min(64) || (t.rowLoads < 4 && split_min(128))))
+                return d;
+            if (t.rowLoads == 1 && !split(2, 256) && !split(1, 512) && split_min(64))
+                return d;
+        }
+        const int split_opt = h->ryxSplit == 4 ? 1 : h->ryxSplit;
+        const int tw = split_opt == 2 ? 128 : 64;
+        if ((split_opt >= 2 && split_min(tw)) || (split_opt == 1 && split(2, 256)) || split(1, 512))
             return d;  // (ryx_split 0: one 8-wave part where it fits)
         // (round 5, late) one more column per thread when that keeps the row in one workgroup, else
         // the fewest parts, each of the fewest 64-thread multiples that hold it: 1080p -> 1600x900
@@ -1105,10 +1123,10 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
         d.cpt = 2;
         d.parts = 0;
     }
-    const int tw = h->ryxSplit == 2 ? 128 : h->ryxSplit == 3 ? 64 : 256;
-    if (!(h->ryxSplit >= 2 && split_min(tw)) &&
-        !(h->ryxSplit == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
-        !(h->ryxSplit == 1 && split(4, 256)))
+    const int sopt = h->ryxSplit == 4 ? 1 : h->ryxSplit;  // (4: the general rows' previous rule, above)
+    const int tw = sopt == 2 ? 128 : sopt == 3 ? 64 : 256;
+    if (!(sopt >= 2 && split_min(tw)) && !(sopt == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
+        !(sopt == 1 && split(4, 256)))
         split_min(512);
     // adjacent column pairs per thread (9:4 only, where every pair's windows start 1 or 2 pairs
     // apart, i.e. columns at 2:1 or more): one LDS run of NP + 2 dwords for both columns
@@ -1611,7 +1629,8 @@ int iqo_hip_plan_set_option(iqo_hip_plan *h, const char *key, long value)
         return IQO_HIP_OK;
     }
     if (!std::strcmp(key, "ryx_split")) {  // ratio-Y kernel column parts (speed only): 0 one 8-wave
-        if (value < 0 || value > 3)          // workgroup per row where it fits, 1 default, 2 / 3 parts of 2 / 1 waves
+        if (value < 0 || value > 4)          // workgroup per row where it fits, 1 default, 2 / 3 parts of 2 / 1 waves,
+                                             // 4 the general rows' round-6 rule before one-wave parts
             return IQO_HIP_EINVAL;
         h->ryxSplit = static_cast<int>(value);
         return IQO_HIP_OK;

@@ -2608,7 +2608,10 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
         // (round 6: ~3 rounds at 4 rows per output row, whose 22-24-row windows make a band's halo
         // costly -- 4K -> 1024x576 x128: 6 bands 0.485 ms, 12 bands 0.494, 18 0.506,
         // profiles/r06/c4_xcd_order.txt)
-        const int rounds = d.nl >= 4 ? 3 : 6;
+        // ryu_kernel (upscale rows by window position) likewise ~3 rounds: 1024x576 -> 1080p x256
+        // 18 bands 0.259 ms, 9 bands 0.248, 6 bands 0.248; 1366x768 -> 1080p 0.285 / 0.269 / 0.269
+        // (profiles/r06/band_sweeps.txt)
+        const int rounds = d.nl >= 4 || byPos ? 3 : 6;
         bands = static_cast<int>(std::min<int64_t>((rounds * resident + perBand - 1) / perBand, std::max(1, rows / 32)));
     }
     bands = std::max(1, std::min(bands, rows));

@@ -40,12 +40,18 @@ def main():
     ap.add_argument("--arm", action="append", default=[])
     ap.add_argument("--trace", action="store_true", help="print the settle phase's per-launch ms")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--shape", default="", help="method,degree,srcW,srcH,dstW,dstH,frames instead of --config")
     args = ap.parse_args()
     import torch
 
     import libiqo_amd
 
-    m, d, sw, sh, dw, dh, px, default_frames, label = bench.CONFIGS[args.config]
+    if args.shape:
+        f = args.shape.split(",")
+        m, (d, sw, sh, dw, dh, default_frames), px = f[0], map(int, f[1:7]), 1
+        args.config = "%s%d:%dx%d->%dx%d" % (m, d, sw, sh, dw, dh)
+    else:
+        m, d, sw, sh, dw, dh, px, default_frames, label = bench.CONFIGS[args.config]
     frames = args.frames or default_frames
     dev = torch.device("cuda", 0)
     arms = []
