@@ -1123,11 +1123,23 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
         d.cpt = 2;
         d.parts = 0;
     }
-    const int sopt = h->ryxSplit == 4 ? 1 : h->ryxSplit;  // (4: the general rows' previous rule, above)
+    const int sopt = h->ryxSplit == 4 ? 1 : h->ryxSplit;  // (4: the previous rules, above and here)
     const int tw = sopt == 2 ? 128 : sopt == 3 ? 64 : 256;
     if (!(sopt >= 2 && split_min(tw)) && !(sopt == 1 && d.lanczos && d.dstW >= 64 && split(2, 256)) && !split(1, 512) &&
         !(sopt == 1 && split(4, 256)))
         split_min(512);
+    // (round 6, late) Lanczos rows whose parts are less than 3/4 busy take the fewest parts of one
+    // wave instead: 2560 columns in four 256-thread parts left 96 threads of each idle (2560x1440 ->
+    // 640x360 0.299 -> 0.240 ms, Lanczos-2 -> 1138x640 0.319 -> 0.263, Lanczos-6 -> 720p 0.235 ->
+    // 0.191); the 1080p / 4K rows of the bench list fill their parts to 94-97 % and keep them (there
+    // one-wave parts were 5-10 % slower), profiles/r06/ryg_split.txt
+    if (h->ryxSplit == 1 && d.lanczos && d.parts > 0) {
+        int busy = 0;
+        for (int k = 0; k < d.parts; ++k)
+            busy += std::max((d.ce[k] - d.cs[k] + 3) / 4, (d.xs[k + 1] - d.xs[k] + d.cpt - 1) / d.cpt);
+        if (4 * busy < 3 * d.parts * d.threads)
+            split_min(64);  // (leaves the split as it is when no one-wave split holds the row)
+    }
     // adjacent column pairs per thread (9:4 only, where every pair's windows start 1 or 2 pairs
     // apart, i.e. columns at 2:1 or more): one LDS run of NP + 2 dwords for both columns
     d.adj = 0;
