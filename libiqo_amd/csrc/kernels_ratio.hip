@@ -2428,6 +2428,7 @@ hipError_t launch_ryx(const RyxDev &d, const Io &io, int rowBegin, int rowEnd, i
         IQO_RYX2(true, 9, 4, 8, 6, 2), IQO_RYX2(true, 9, 4, 8, 7, 2),     // Lanczos-2 9:4
         IQO_RYX2(false, 9, 4, 4, 3, 2),                                   // Area 9:4
         IQO_RYX(true, 4, 1, 14, 13, 4), IQO_RYX(true, 4, 1, 14, 9, 4),  // Lanczos-3 / -2 4:1 (4K -> 960x540)
+        IQO_RYX(true, 4, 1, 22, 17, 3),  // Lanczos-4 4:1 (round 6: 22 of 32 row taps; had run the general kernel)
         IQO_RYX(true, 2, 1, 4, 3, 2),                                   // Lanczos-1 2:1
         IQO_RYX(true, 2, 1, 12, 9, 3), IQO_RYX(true, 2, 1, 16, 11, 4),  // Lanczos-4 / -5 2:1
         IQO_RYX(true, 2, 1, 18, 13, 5), IQO_RYX(true, 2, 1, 20, 15, 5), // Lanczos-6 / -7 2:1

@@ -1455,7 +1455,7 @@ void build_ryx(const Plan &p, RyxTables *t)
     };
     static const Shape kShapes[] = {{kLanczos, 9, 4, 12, 8},  {kLanczos, 9, 4, 12, 10}, {kLanczos, 9, 4, 8, 6},
                                     {kLanczos, 9, 4, 8, 7},   {kArea, 9, 4, 4, 3},      {kLanczos, 4, 1, 14, 9},
-                                    {kLanczos, 4, 1, 14, 13}, {kLanczos, 2, 1, 4, 3},   {kLanczos, 2, 1, 12, 9},
+                                    {kLanczos, 4, 1, 14, 13}, {kLanczos, 4, 1, 22, 17}, {kLanczos, 2, 1, 4, 3},   {kLanczos, 2, 1, 12, 9},
                                     {kLanczos, 2, 1, 16, 11}, {kLanczos, 2, 1, 18, 13}, {kLanczos, 2, 1, 20, 15},
                                     {kLanczos, 2, 1, 22, 17}, {kLanczos, 2, 1, 24, 19}, {kLanczos, 4, 9, 6, 4},
                                     {kLanczos, 4, 9, 4, 3}};

@@ -84,6 +84,7 @@ def _shapes():
            ("linear_up", "linear", 0, 1280, 720, 3840, 2160), ("linear_up", "linear", 0, 1920, 1080, 3840, 2160),
            ("linear_up", "linear", 0, 8, 2, 24, 6), ("linear_up", "linear", 0, 16, 3, 32, 6),
            ("ryx", "lanczos", 3, 3840, 2160, 960, 540), ("ryx", "lanczos", 2, 1920, 1080, 480, 270),  # 4:1
+           ("ryx", "lanczos", 4, 2560, 1440, 640, 360), ("ryx", "lanczos", 4, 1000, 600, 250, 150),  # 4:1 Lanczos-4
            ("ryx", "lanczos", 1, 640, 480, 320, 240), ("ryx", "lanczos", 4, 1920, 1080, 960, 540),   # 2:1
            ("ryx", "lanczos", 5, 640, 360, 320, 180), ("ryx", "lanczos", 6, 640, 360, 320, 180),
            ("ryx", "lanczos", 7, 720, 480, 360, 240), ("ryx", "lanczos", 8, 640, 360, 320, 180),
