@@ -2536,6 +2536,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
 #define IQO_RYG(LZ_, T_, NP_) IQO_RYG_N(LZ_, T_, NP_, 2)
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
+                                 IQO_RYG(true, 12, 8),  // (round 6: Lanczos-5 rows of 1 .. 2 : 1, 8 column pairs)
                                  // upscales (windows 0 or 1 rows apart: one new row per output row)
                                  IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1), IQO_RYG_N(true, 8, 5, 1),
                                  // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)
@@ -2546,6 +2547,8 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  {true, 14, 8, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 14, 8, kRygPD, 2, 3>), 0, 0},
                                  {true, 16, 9, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 16, 9, kRygPD, 2, 3>), 0, 0},
                                  {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 3>), 0, 0},
+                                 // (round 6: Lanczos-4 rows of 2 .. 3 : 1, 12 column pairs: 4K -> 1366x768 had run the tile kernel)
+                                 {true, 18, 12, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 12, kRygPD, 2, 3>), 0, 0},
                                  // Area downscales of 2 .. 3 : 1
                                  {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, kRygPD, 2, 3>), 0, 0},
                                  {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, kRygPD, 2, 3>), 0, 0},
