@@ -1229,9 +1229,9 @@ struct RygArgs {
 
 // (occupancy: two 512-thread workgroups per CU up to 22 row taps -- at 22 the compiler spills a few
 // registers and the kernel is still 5.5 % faster than at one workgroup per CU, 4K -> 1024x576
-// profiles/r05/steady_ryg_wpe.txt; 24 taps stay at one)
+// profiles/r05/steady_ryg_wpe.txt; 24 taps and Lanczos-4's 16 column pairs stay at one)
 template <bool LZ, int T, int NP, int PD, int CPT, int NL>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 22 ? 2 : 4))) void ryg_kernel(RygArgs a)
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(T > 22 || NP > 13 ? 2 : 4))) void ryg_kernel(RygArgs a)
 {
     static_assert(CPT >= 2 && CPT <= 4, "output columns per thread");
     static_assert(NL >= 1 && NL <= 4, "rows loaded per output row: 1 (upscales), 2 .. 4 (down to 2:1 .. 4:1)");
@@ -2559,6 +2559,8 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  {true, 20, 11, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 20, 11, kRygPD, 2, 4>), 0, 0},
                                  {true, 22, 12, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 12, kRygPD, 2, 4>), 0, 0},
                                  {true, 24, 13, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 24, 13, kRygPD, 2, 4>), 0, 0},
+                                 // (round 6: Lanczos-4 rows of 3 .. 4 : 1, 16 column pairs, one workgroup per CU)
+                                 {true, 22, 16, 2, 4, reinterpret_cast<const void *>(ryg_kernel<true, 22, 16, kRygPD, 2, 4>), 0, 0},
                                  {false, 5, 3, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 3, kRygPD, 2, 4>), 0, 0},
                                  {false, 5, 4, 2, 4, reinterpret_cast<const void *>(ryg_kernel<false, 5, 4, kRygPD, 2, 4>), 0, 0}};
 #undef IQO_RYG_N
