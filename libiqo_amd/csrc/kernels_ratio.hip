@@ -2537,6 +2537,7 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
     static const Inst kInst[] = {IQO_RYG(true, 4, 3),  IQO_RYG(true, 6, 4),  IQO_RYG(true, 8, 5),  IQO_RYG(true, 10, 5),
                                  IQO_RYG(true, 10, 6), IQO_RYG(true, 12, 7),
                                  IQO_RYG(true, 12, 8),  // (round 6: Lanczos-5 rows of 1 .. 2 : 1, 8 column pairs)
+                                 IQO_RYG(true, 16, 10), IQO_RYG(true, 16, 12),  // (round 6: Lanczos-5 / -6 rows of 1 .. 2 : 1)
                                  // upscales (windows 0 or 1 rows apart: one new row per output row)
                                  IQO_RYG_N(true, 4, 3, 1), IQO_RYG_N(true, 6, 4, 1), IQO_RYG_N(true, 8, 5, 1),
                                  // Area downscales of 1 .. 2 : 1 (round 5: after the ring and the columns-per-thread rule)

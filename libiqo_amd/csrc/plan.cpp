@@ -1596,16 +1596,16 @@ void build_ryg(const Plan &p, RyxTables *t)
                                     {kLanczos, 14, 8}, {kLanczos, 16, 9}, {kLanczos, 18, 10}, {kArea, 4, 3},
                                     {kArea, 4, 4},     {kLanczos, 20, 11}, {kLanczos, 22, 12}, {kLanczos, 24, 13},
                                     {kArea, 5, 3},     {kArea, 5, 4},     {kLanczos, 12, 8}, {kLanczos, 18, 12},
-                                    {kLanczos, 22, 16}};
+                                    {kLanczos, 22, 16}, {kLanczos, 16, 10}, {kLanczos, 16, 12}};
     const int needNP = ryx_column_pairs(p);
     const Shape *best = nullptr;
     for (const Shape &S : kShapes)
         if (S.method == sm && S.T >= TE && S.T <= T + (linear ? 1 : 0) && needNP <= S.NP && (!up || S.T <= 8) &&
             // (kernels.hip instantiations: NL = 3 Lanczos (T, T/2 + 1) for T 10 .. 18 and Area (4, 3 / 4);
-            // and (18, 12) (round 6, Lanczos-4); NL = 4 (T, T/2 + 1) for T 14 .. 24 and (22, 16); NL = 2 up to 12 taps, (12, 8) for Lanczos-5; NL = 1 Lanczos 4, 6, 8 taps)
+            // and (18, 12) (round 6, Lanczos-4); NL = 4 (T, T/2 + 1) for T 14 .. 24 and (22, 16); NL = 2 up to 12 taps, (12, 8) for Lanczos-5, (16, 10 / 12) for Lanczos-5 / -6; NL = 1 Lanczos 4, 6, 8 taps)
             (maxAdv == 4   ? (sm == kArea ? S.T == 5 : S.T >= 14 && (S.NP == S.T / 2 + 1 || (S.T == 22 && S.NP == 16)))
              : maxAdv == 3 ? (sm == kArea ? S.T == 4 : S.T >= 10 && S.T <= 18 && (S.NP == S.T / 2 + 1 || (S.T == 18 && S.NP == 12)))
-                           : S.T <= 12 && !(sm == kArea && S.T >= 4)) &&
+                           : (S.T <= 12 || (S.T == 16 && S.NP >= 10)) && !(sm == kArea && S.T >= 4)) &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;
     if (!best)
