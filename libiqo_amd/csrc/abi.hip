@@ -1081,8 +1081,10 @@ iqo_amd::RyxDev ryx_dev(const iqo_hip_plan *h)
     // 0.308 (a third of the threads idle in the horizontal pass), 2 columns needed four parts
     // (profiles/r05/steady_ryg_cpt.txt); option "ryg_cpt" forces 2, 3 or 4
     if (t.general) {
-        const int cap = t.taps >= 12 || t.NP >= 6 ? 3 : 4;  // (12-row windows or 6 column pairs with 4
-                                                            // columns per thread spill: 3 at most there)
+        // (12-row windows or 6 column pairs with 4 columns per thread spill: 3 at most there; 16-row
+        // windows spill at 3: 2 there, Lanczos-6 1080p -> 1366x768 0.490 -> 0.381 ms,
+        // profiles/r06/ryg_l45.txt)
+        const int cap = t.taps >= 16 ? 2 : t.taps >= 12 || t.NP >= 6 ? 3 : 4;
         d.cpt = h->rygCpt ? h->rygCpt : std::min(cap, std::max(2, (4 * d.dstW + d.srcW / 2) / d.srcW));
         if (t.rowLoads >= 3)
             d.cpt = 2;  // (downscales past 2:1: 2 columns per thread is the only instantiation)
