@@ -2550,6 +2550,8 @@ hipError_t launch_ryg(const RygDev &d, const Io &io, int rowBegin, int rowEnd, i
                                  {true, 18, 10, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 10, kRygPD, 2, 3>), 0, 0},
                                  // (round 6: Lanczos-4 rows of 2 .. 3 : 1, 12 column pairs: 4K -> 1366x768 had run the tile kernel)
                                  {true, 18, 12, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 18, 12, kRygPD, 2, 3>), 0, 0},
+                                 // (round 6: Lanczos-5 rows of 2 .. 3 : 1, 22 taps, 16 column pairs, one workgroup per CU)
+                                 {true, 22, 16, 2, 3, reinterpret_cast<const void *>(ryg_kernel<true, 22, 16, kRygPD, 2, 3>), 0, 0},
                                  // Area downscales of 2 .. 3 : 1
                                  {false, 4, 3, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 3, kRygPD, 2, 3>), 0, 0},
                                  {false, 4, 4, 2, 3, reinterpret_cast<const void *>(ryg_kernel<false, 4, 4, kRygPD, 2, 3>), 0, 0},

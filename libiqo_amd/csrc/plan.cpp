@@ -1602,9 +1602,11 @@ void build_ryg(const Plan &p, RyxTables *t)
     for (const Shape &S : kShapes)
         if (S.method == sm && S.T >= TE && S.T <= T + (linear ? 1 : 0) && needNP <= S.NP && (!up || S.T <= 8) &&
             // (kernels.hip instantiations: NL = 3 Lanczos (T, T/2 + 1) for T 10 .. 18 and Area (4, 3 / 4);
-            // and (18, 12) (round 6, Lanczos-4); NL = 4 (T, T/2 + 1) for T 14 .. 24 and (22, 16); NL = 2 up to 12 taps, (12, 8) for Lanczos-5, (16, 10 / 12) for Lanczos-5 / -6; NL = 1 Lanczos 4, 6, 8 taps)
+            // and (18, 12), (22, 16) (round 6, Lanczos-4 / -5); NL = 4 (T, T/2 + 1) for T 14 .. 24 and (22, 16); NL = 2 up to 12 taps, (12, 8) for Lanczos-5, (16, 10 / 12) for Lanczos-5 / -6; NL = 1 Lanczos 4, 6, 8 taps)
             (maxAdv == 4   ? (sm == kArea ? S.T == 5 : S.T >= 14 && (S.NP == S.T / 2 + 1 || (S.T == 22 && S.NP == 16)))
-             : maxAdv == 3 ? (sm == kArea ? S.T == 4 : S.T >= 10 && S.T <= 18 && (S.NP == S.T / 2 + 1 || (S.T == 18 && S.NP == 12)))
+             : maxAdv == 3 ? (sm == kArea ? S.T == 4
+                                           : (S.T >= 10 && S.T <= 18 && (S.NP == S.T / 2 + 1 || (S.T == 18 && S.NP == 12))) ||
+                                                 (S.T == 22 && S.NP == 16))
                            : (S.T <= 12 || (S.T == 16 && S.NP >= 10)) && !(sm == kArea && S.T >= 4)) &&
             (!best || S.T < best->T || (S.T == best->T && S.NP < best->NP)))  // (upscales: kernels.hip NL = 1 shapes)
             best = &S;

@@ -100,6 +100,7 @@ def _shapes():
            ("ryg", "lanczos", 4, 3840, 2160, 1366, 768), ("ryg", "lanczos", 5, 1920, 1080, 1366, 768),  # round 6
            ("ryg", "lanczos", 4, 3840, 2160, 1024, 576), ("ryg", "lanczos", 4, 1920, 1080, 512, 288),
            ("ryg", "lanczos", 6, 1920, 1080, 1366, 768), ("ryg", "lanczos", 5, 1920, 1080, 854, 600),
+           ("ryg", "lanczos", 5, 3840, 2160, 1366, 768),
            ("ryg", "area", 0, 3840, 2160, 1366, 768), ("ryg", "lanczos", 4, 1024, 576, 1920, 1080),
            ("ryg", "lanczos", 3, 1367, 769, 1920, 1080), ("ryg", "lanczos", 2, 1918, 1078, 1366, 768),
            # general upscale rows by window position (ryu, round 6): 15:8, 45:32, Lanczos-2/4, odd sizes
