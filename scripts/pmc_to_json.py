@@ -28,7 +28,7 @@ BENCH = {"c2": ("lanczos_stream", 1024), "c3": ("area_int", 64), "c4": ("linear_
          "h5": ("linear_up2", 64), "h6": ("ryx", 128),
          # round 6: the general-row kernels (upscale rows on ryu_kernel, 3..4:1 downscale rows on ryg_kernel)
          "u1": ("ryx", 256), "u2": ("ryg", 256, "ryu_kernel"), "u3": ("ryg", 256, "ryu_kernel"),
-         "w6": ("ryg", 128, "ryg_kernel")}
+         "w6": ("ryg", 128, "ryg_kernel"), "w4": ("ryg", 128, "ryg_kernel"), "w1": ("ryg", 256, "ryg_kernel")}
 
 
 def per_dispatch(dirname, counter, kname):
